@@ -1,0 +1,207 @@
+/*
+ * rpkt_gpu.h — C ABI of the MI355X packet-batch parse + checksum engine.
+ *
+ * This is the drop-in boundary for rpkt's Ether -> (802.1Q/802.1ad)* -> IPv4 ->
+ * {TCP, UDP} decode-and-verify path.  rpkt itself has no FFI for this path: its
+ * "operator API" is the generic header views over `T: Buf`
+ *   EtherFrame::parse      rpkt/src/ether/generated.rs:34-41
+ *   VlanFrame::parse       rpkt/src/vlan/generated.rs:32-39
+ *   Ipv4::parse            rpkt/src/ipv4/generated.rs:35-51
+ *   Udp::parse             rpkt/src/udp/generated.rs:31-42
+ *   Tcp::parse             rpkt/src/tcp/generated.rs:34-45
+ *   checksum::from_slice   rpkt/src/checksum.rs:33-62
+ *   checksum::combine      rpkt/src/checksum.rs:68-74
+ * which a caller drives one frame at a time (benches/rpkt/rpkt_parse.rs:62-80,
+ * rpkt-dpdk/examples/loopback_rx.rs:96-121).  The entry points below replace that
+ * per-frame loop with one call over a device-resident batch of frames, and return
+ * one fixed-size record per frame holding every getter value the chain above
+ * exposes, the parse outcome and the raw RFC 1071 sums.
+ *
+ * Conventions (no HIP/torch types cross this header):
+ *   - every pointer named *_dev is device memory owned by the caller;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream);
+ *   - calls are asynchronous on `stream` and never allocate or synchronise;
+ *   - API-level failures are negative return codes; per-frame parse failures are
+ *     never errors, they are reported in rpkt_rec_t.status.
+ */
+#ifndef RPKT_GPU_H
+#define RPKT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RPKT_ABI_VERSION 1u
+
+/* ---- per-frame status: which rpkt `parse` would return Err (first one) ----
+ * The chain is EtherFrame::parse -> while ethertype in {VLAN, QINQ}:
+ * VlanFrame::parse -> (ethertype == IPV4) -> Ipv4::parse -> protocol dispatch ->
+ * Udp::parse | Tcp::parse.  At most RPKT_MAX_VLAN tags are walked; a further
+ * tag leaves the dispatch ethertype at 0x8100/0x88a8 -> RPKT_S_NOT_IPV4. */
+enum rpkt_status {
+    RPKT_S_OK = 0,              /* Udp::parse or Tcp::parse returned Ok           */
+    RPKT_S_ETH_SHORT = 1,       /* chunk_len < 14     ether/generated.rs:36        */
+    RPKT_S_VLAN_SHORT = 2,      /* chunk_len < 4      vlan/generated.rs:34         */
+    RPKT_S_NOT_IPV4 = 3,        /* ethertype != 0x0800 (caller check, rpkt_parse.rs:66) */
+    RPKT_S_IP_SHORT = 4,        /* chunk_len < 20     ipv4/generated.rs:37         */
+    RPKT_S_IP_BAD_IHL = 5,      /* header_len < 20    ipv4/generated.rs:43         */
+    RPKT_S_IP_IHL_GT_LEN = 6,   /* header_len > chunk_len   ipv4/generated.rs:44   */
+    RPKT_S_IP_TOT_LT_IHL = 7,   /* packet_len < header_len  ipv4/generated.rs:45   */
+    RPKT_S_IP_TOT_GT_LEN = 8,   /* packet_len > remaining   ipv4/generated.rs:46   */
+    RPKT_S_L4_OTHER = 9,        /* IPv4 ok, protocol not TCP(6)/UDP(17)            */
+    RPKT_S_UDP_SHORT = 10,      /* chunk_len < 8      udp/generated.rs:33          */
+    RPKT_S_UDP_BAD_LEN = 11,    /* len < 8 || len > remaining  udp/generated.rs:38 */
+    RPKT_S_TCP_SHORT = 12,      /* chunk_len < 20     tcp/generated.rs:36          */
+    RPKT_S_TCP_BAD_DOFF = 13    /* hlen < 20 || hlen > chunk_len  tcp/generated.rs:41 */
+};
+
+#define RPKT_MAX_VLAN 2
+
+/* ---- API return codes ---- */
+enum rpkt_err {
+    RPKT_OK = 0,
+    RPKT_E_INVAL = -1,       /* NULL pointer / zero stride / bad flags            */
+    RPKT_E_HIP = -2,         /* a HIP runtime call failed (see rpkt_gpu_last_hip_error) */
+    RPKT_E_TOO_LARGE = -3,   /* frames_bytes >= 4 GiB: split the batch             */
+    RPKT_E_ALIGN = -4        /* out/flow buffer not 16-byte aligned               */
+};
+
+/* ---- flags for rpkt_gpu_parse_batch ---- */
+enum rpkt_flags {
+    RPKT_F_IP_SUM = 1u,      /* compute ip_sum = from_slice(ipv4 header[0..ihl4])  */
+    RPKT_F_L4_SUM = 2u,      /* compute l4_sum = combine(pseudo, from_slice(l4))    */
+    RPKT_F_FLOW_EV = 4u      /* also write one rpkt_flow_ev_t per frame             */
+};
+
+/* Record layout: 80 bytes, 16-byte aligned, little-endian host order.
+ * Field  <-> rpkt getter (all getters of the path are recoverable exactly):
+ *   ethertype          EtherFrame::ethertype          ether/generated.rs:55-59
+ *   dst_addr/src_addr  EtherFrame::{dst,src}_addr     ether/generated.rs:47-54
+ *   vlan_tci[i]        be16[0..2] of tag i: priority = tci>>13, dei = tci&0x1000,
+ *                      vlan_id = tci&0xfff            vlan/generated.rs:45-56
+ *   vlan_ethertype[i]  VlanFrame::ethertype           vlan/generated.rs:57-61
+ *   ip_vhl             byte 0: version = >>4, header_len = (&0xf)*4
+ *   ip_tos             byte 1: dscp = >>2, ecn = &3
+ *   ip_frag            be16[6..8]: flag_reserved = >>15, dont_frag = &0x4000,
+ *                      more_frag = &0x2000, frag_offset = &0x1fff
+ *                      (Ipv4 getters ipv4/generated.rs:61-112, 269-288)
+ *   l4_word6           TCP: be16[12..14] (header_len = (>>12)*4, reserved =
+ *                      (>>8)&0xf, flags = &0xff); UDP: packet_len be16[4..6]
+ *   l4_checksum        TCP be16[16..18] / UDP be16[6..8]
+ *   tcp_*              Tcp getters tcp/generated.rs:55-122
+ *   l3_off             frame offset of the IPv4 header (EtherFrame/VlanFrame::payload)
+ *   l4_off             frame offset of Ipv4::payload() (trimmed to packet_len)
+ *   payload_off/_len   Udp::payload() / Tcp::payload() when status == OK,
+ *                      otherwise Ipv4::payload() when IPv4 parsed
+ *   ip_sum             checksum::from_slice(ipv4[0..header_len]); 0xffff <=> valid
+ *   l4_sum             checksum::combine(&[pseudo(src,dst,proto,l4_len),
+ *                      from_slice(l4[0..l4_len])]); 0xffff <=> valid
+ * Fields of layers that were not reached are zero.  Sums not requested by the
+ * flags, or whose layer did not parse, are zero. */
+typedef struct rpkt_rec {
+    uint8_t  status;            /*  0 enum rpkt_status                          */
+    uint8_t  n_vlan;            /*  1 tags walked, 0..RPKT_MAX_VLAN             */
+    uint16_t ethertype;         /*  2                                           */
+    uint8_t  dst_addr[6];       /*  4                                           */
+    uint8_t  src_addr[6];       /* 10                                           */
+    uint16_t vlan_tci[2];       /* 16                                           */
+    uint16_t vlan_ethertype[2]; /* 20                                           */
+    uint8_t  ip_vhl;            /* 24                                           */
+    uint8_t  ip_tos;            /* 25                                           */
+    uint16_t ip_packet_len;     /* 26                                           */
+    uint16_t ip_ident;          /* 28                                           */
+    uint16_t ip_frag;           /* 30                                           */
+    uint8_t  ip_ttl;            /* 32                                           */
+    uint8_t  ip_protocol;       /* 33                                           */
+    uint16_t ip_checksum;       /* 34                                           */
+    uint32_t ip_src;            /* 36 a.b.c.d -> (a<<24)|(b<<16)|(c<<8)|d        */
+    uint32_t ip_dst;            /* 40                                           */
+    uint16_t src_port;          /* 44                                           */
+    uint16_t dst_port;          /* 46                                           */
+    uint32_t tcp_seq;           /* 48                                           */
+    uint32_t tcp_ack;           /* 52                                           */
+    uint16_t l4_word6;          /* 56                                           */
+    uint16_t tcp_window;        /* 58                                           */
+    uint16_t l4_checksum;       /* 60                                           */
+    uint16_t tcp_urgent;        /* 62                                           */
+    uint16_t l3_off;            /* 64                                           */
+    uint16_t l4_off;            /* 66                                           */
+    uint16_t payload_off;       /* 68                                           */
+    uint16_t payload_len;       /* 70                                           */
+    uint16_t ip_sum;            /* 72                                           */
+    uint16_t l4_sum;            /* 74                                           */
+    uint32_t frame_len;         /* 76 Cursor::remaining() of the whole frame    */
+} rpkt_rec_t;
+
+#define RPKT_REC_BYTES 80u
+
+/* Per-frame flow event (RPKT_F_FLOW_EV), 8 bytes:
+ *   bits  0..31  frame_len
+ *   bits 32..47  flow bucket = rpkt_flow_hash(5-tuple) % n_buckets (status OK),
+ *                n_buckets for frames that did not parse to L4
+ *   bit  48      ip header sum != 0xffff
+ *   bit  49      l4 sum != 0xffff (a UDP checksum field of 0 counts as valid)
+ * Counters (rpkt_gpu_flow_count) are u64[(n_buckets + 1) * 4]:
+ *   row b = {pkts, bytes, ip_bad, l4_bad}; row n_buckets = unparsed frames. */
+typedef uint64_t rpkt_flow_ev_t;
+#define RPKT_FLOW_MAX_BUCKETS 65535u
+
+/* Frame batch descriptor.  Frame i is [off_i, off_i + len_i) of `frames_dev`:
+ *   packed  (offsets_dev != NULL): off_i = offsets[i], len_i = offsets[i+1] - offsets[i]
+ *                                  (n + 1 entries, non-decreasing);
+ *   strided (offsets_dev == NULL): off_i = i * stride, len_i = frame_len (0 -> stride).
+ * Loads are bounds-checked in hardware against frames_bytes, so a malformed
+ * descriptor yields wrong records, never a fault.  frames_bytes < 4 GiB. */
+typedef struct rpkt_batch {
+    const uint8_t*  frames_dev;
+    uint64_t        frames_bytes;
+    const uint32_t* offsets_dev;
+    uint32_t        stride;
+    uint32_t        frame_len;
+    uint32_t        n;
+    uint32_t        reserved;
+} rpkt_batch_t;
+
+/* ABI version and build information (host-only, no device calls). */
+uint32_t rpkt_gpu_abi_version(void);
+const char* rpkt_gpu_build_info(void);
+const char* rpkt_gpu_status_name(int status);
+/* Last HIP error code seen by this thread (hipError_t as int), 0 if none. */
+int rpkt_gpu_last_hip_error(void);
+
+/* Parse + verify a batch.  Replaces, per frame i, the reference sequence
+ *   EtherFrame::parse -> [VlanFrame::parse]* -> Ipv4::parse -> Udp|Tcp::parse
+ * plus the checksum composition selected by `flags`, writing recs_dev[i]
+ * (n * 80 bytes, 16-byte aligned).  flow_ev_dev (n * 8 bytes) is written when
+ * RPKT_F_FLOW_EV is set, using n_buckets (1..RPKT_FLOW_MAX_BUCKETS). */
+int rpkt_gpu_parse_batch(const rpkt_batch_t* batch, uint32_t flags,
+                         rpkt_rec_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
+                         uint32_t n_buckets, void* stream);
+
+/* Accumulate flow events into counters_dev (u64[(n_buckets+1)*4], caller
+ * zeroes it once; calls add).  workspace_dev must hold
+ * rpkt_gpu_flow_workspace_bytes(n, n_buckets) bytes. */
+size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets);
+int rpkt_gpu_flow_count(const rpkt_flow_ev_t* flow_ev_dev, uint32_t n,
+                        uint32_t n_buckets, uint64_t* counters_dev,
+                        void* workspace_dev, void* stream);
+
+/* Batched checksum::from_slice over byte ranges of a device buffer:
+ * out_dev[i] = from_slice(buf[start_i .. start_i + len_i]) for
+ * ranges_dev[i] = {start_i, len_i}.  Drop-in for rpkt/src/checksum.rs:33-62. */
+int rpkt_gpu_checksum_ranges(const uint8_t* buf_dev, uint64_t buf_bytes,
+                             const uint32_t* ranges_dev, uint32_t n,
+                             uint16_t* out_dev, void* stream);
+
+/* 5-tuple hash used for flow buckets (host copy of the device function). */
+uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,
+                        uint16_t dst_port, uint8_t protocol);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RPKT_GPU_H */

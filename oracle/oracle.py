@@ -1,0 +1,126 @@
+"""ctypes wrapper of the CPU oracle (oracle/_build/librpkt_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker.  Nothing in rpkt_amd/ imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "librpkt_oracle.so")
+
+_lib = None
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc, seconds)."""
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oracle_from_slice.argtypes = [u8p, ctypes.c_size_t]
+        L.oracle_from_slice.restype = ctypes.c_uint16
+        L.oracle_combine.argtypes = [ctypes.POINTER(ctypes.c_uint16), ctypes.c_size_t]
+        L.oracle_combine.restype = ctypes.c_uint16
+        L.oracle_from_buf.argtypes = [ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.c_size_t, ctypes.c_size_t]
+        L.oracle_from_buf.restype = ctypes.c_uint16
+        L.oracle_parse_one.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_void_p]
+        L.oracle_parse_one.restype = None
+        L.oracle_parse_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+        L.oracle_parse_batch.restype = None
+        L.oracle_parse_batch_mt.argtypes = L.oracle_parse_batch.argtypes + [ctypes.c_int]
+        L.oracle_parse_batch_mt.restype = ctypes.c_int
+        L.oracle_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
+                                       ctypes.c_uint16, ctypes.c_uint8]
+        L.oracle_flow_hash.restype = ctypes.c_uint32
+        L.oracle_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p]
+        L.oracle_flow_count.restype = None
+        L.oracle_packet_l4.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint16,
+                                       ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
+                                       ctypes.c_uint16]
+        L.oracle_packet_l4.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def from_slice(data):
+    b = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    b = np.ascontiguousarray(b, dtype=np.uint8)
+    return int(lib().oracle_from_slice(b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), b.size))
+
+
+def combine(words):
+    a = (ctypes.c_uint16 * len(words))(*words)
+    return int(lib().oracle_combine(a, len(words)))
+
+
+def from_buf(segments, length=None):
+    segs = [np.ascontiguousarray(np.frombuffer(bytes(s), dtype=np.uint8)) for s in segments]
+    total = sum(s.size for s in segs)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    ptrs = (u8p * len(segs))(*[s.ctypes.data_as(u8p) for s in segs])
+    lens = (ctypes.c_size_t * len(segs))(*[s.size for s in segs])
+    return int(lib().oracle_from_buf(ptrs, lens, len(segs), total if length is None else length))
+
+
+def parse_one(frame, flags=3):
+    from rpkt_amd.records import REC_DTYPE
+    b = np.ascontiguousarray(np.frombuffer(bytes(frame), dtype=np.uint8))
+    rec = np.zeros(1, dtype=REC_DTYPE)
+    lib().oracle_parse_one(_ptr(b), b.size, flags, _ptr(rec))
+    return rec[0]
+
+
+def parse_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0, n_buckets=0,
+                threads=1, flow_ev=False):
+    """Oracle records (and optionally flow events) for a host batch."""
+    from rpkt_amd.records import REC_DTYPE
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    ev = np.zeros(n, dtype=np.uint64) if flow_ev else None
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    if threads > 1:
+        lib().oracle_parse_batch_mt(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
+                                    flags, n_buckets, _ptr(recs), _ptr(ev), threads)
+    else:
+        lib().oracle_parse_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
+                                 flags, n_buckets, _ptr(recs), _ptr(ev))
+    return (recs, ev) if flow_ev else recs
+
+
+def flow_count(ev, n_buckets):
+    ev = np.ascontiguousarray(ev, dtype=np.uint64)
+    counters = np.zeros((n_buckets + 1) * 4, dtype=np.uint64)
+    lib().oracle_flow_count(_ptr(ev), ev.size, n_buckets, _ptr(counters))
+    return counters
+
+
+def flow_hash(src, dst, sp, dp, proto):
+    return int(lib().oracle_flow_hash(src, dst, sp, dp, proto))
+
+
+def load_dat(path):
+    """rpkt/tests/common/mod.rs:3-29: hex text, two characters per byte."""
+    with open(path) as fh:
+        s = fh.read().strip()
+    return bytes(int(s[i:i + 2], 16) for i in range(0, len(s), 2))

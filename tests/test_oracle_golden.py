@@ -1,0 +1,186 @@
+"""Pin the CPU oracle against the reference's own fixtures and asserted values.
+
+Each check below restates an assert from the reference's tests (cited in
+tests/golden/expected.json) or a checksum property of the captured frames.
+Runs on CPU only.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from rpkt_amd.records import STATUS
+from rpkt_amd.views import EtherFrame, VlanFrame, Ipv4, Udp, Tcp, Packet, EtherType, IpProtocol
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+PKTS = os.path.join(GOLD, "packets")
+with open(os.path.join(GOLD, "expected.json")) as fh:
+    EXPECTED = json.load(fh)
+
+# the l4 / ip sums of the offload-captured (invalid) frames.
+APPENDIX_A_INVALID = {
+    "bench_frame.dat": {"ip_sum": 0xde00, "l4_sum": 0xb49d},
+}
+
+
+def derived(rec, key):
+    vhl, frag, w6 = int(rec["ip_vhl"]), int(rec["ip_frag"]), int(rec["l4_word6"])
+    d = {
+        "ip_header_len": (vhl & 0xf) * 4, "ip_version": vhl >> 4,
+        "ip_dscp": int(rec["ip_tos"]) >> 2, "ip_ecn": int(rec["ip_tos"]) & 3,
+        "ip_flag_reserved": frag >> 15, "ip_dont_frag": (frag >> 14) & 1,
+        "ip_more_frag": (frag >> 13) & 1, "ip_frag_offset": frag & 0x1fff,
+        "tcp_header_len": (w6 >> 12) * 4, "tcp_flags": w6 & 0xff,
+        "vlan0_id": int(rec["vlan_tci"][0]) & 0xfff,
+        "vlan0_priority": int(rec["vlan_tci"][0]) >> 13,
+        "vlan0_dei": (int(rec["vlan_tci"][0]) >> 12) & 1,
+        "vlan0_ethertype": int(rec["vlan_ethertype"][0]),
+        "vlan1_id": int(rec["vlan_tci"][1]) & 0xfff,
+        "vlan1_priority": int(rec["vlan_tci"][1]) >> 13,
+        "vlan1_dei": (int(rec["vlan_tci"][1]) >> 12) & 1,
+        "vlan1_ethertype": int(rec["vlan_ethertype"][1]),
+    }
+    if key in d:
+        return d[key]
+    v = rec[key]
+    if isinstance(v, np.ndarray):
+        return [int(x) for x in v]
+    return int(v)
+
+
+@pytest.mark.parametrize("name", sorted(EXPECTED))
+def test_fixture_getters(name):
+    frame = oracle.load_dat(os.path.join(PKTS, name))
+    rec = oracle.parse_one(frame, flags=3)
+    exp = EXPECTED[name]
+    assert int(rec["status"]) == STATUS[exp["status"]], name
+    assert int(rec["frame_len"]) == len(frame)
+    for k, v in exp.items():
+        if k in ("cite", "status", "sums", "l4_sum"):
+            continue
+        assert derived(rec, k) == v, (name, k)
+    sums = exp.get("sums")
+    if sums == "valid":
+        assert int(rec["ip_sum"]) == 0xffff and int(rec["l4_sum"]) == 0xffff, name
+    elif sums == "ip_valid":
+        assert int(rec["ip_sum"]) == 0xffff and int(rec["l4_sum"]) == 0, name
+    elif sums in ("ip_valid_l4_invalid", "ip_valid_udp_zero"):
+        assert int(rec["ip_sum"]) == 0xffff
+        assert int(rec["l4_sum"]) == exp["l4_sum"], name
+    elif sums == "invalid":
+        assert int(rec["ip_sum"]) == APPENDIX_A_INVALID[name]["ip_sum"]
+        assert int(rec["l4_sum"]) == APPENDIX_A_INVALID[name]["l4_sum"]
+
+
+def test_every_fixture_parses_without_abort():
+    for f in sorted(os.listdir(PKTS)):
+        frame = oracle.load_dat(os.path.join(PKTS, f))
+        rec = oracle.parse_one(frame, flags=3)
+        assert int(rec["status"]) in STATUS.values()
+        for cut in range(0, len(frame) + 1, 7):       # every truncation is a clean status
+            r = oracle.parse_one(frame[:cut], flags=3)
+            assert int(r["status"]) in STATUS.values()
+
+
+def test_views_read_like_reference_bench():
+    """benches/rpkt/rpkt_parse.rs:62-106 through the host views."""
+    frame = oracle.load_dat(os.path.join(PKTS, "bench_frame.dat"))
+    rec = oracle.parse_one(frame, flags=3)
+    eth = EtherFrame.parse(Packet(rec, frame)).unwrap()
+    assert eth.ethertype() == EtherType.IPV4
+    assert eth.dst_addr() == frame[0:6] and eth.src_addr() == frame[6:12]
+    ip = Ipv4.parse(eth.payload()).unwrap()
+    assert ip.protocol() == IpProtocol.UDP
+    assert ip.src_addr() == "192.168.29.58" and ip.dst_addr() == "192.168.29.160"
+    assert ip.checksum() == 0x0000 and ip.ident() == 0x5c65
+    udp = Udp.parse(ip.payload()).unwrap()
+    assert udp.src_port() == 60376 and udp.dst_port() == 161
+    assert udp.packet_len() == 74 and udp.checksum() == 0xbc86
+    payload = udp.payload()
+    assert payload.chunk() == frame[42:108]
+    assert Tcp.parse(ip.payload()).is_err()
+    assert not ip.verify_checksum() and not udp.verify_checksum()
+
+
+def test_views_qinq_chain():
+    """rpkt/tests/vlan_mpls_tests.rs:96-130 through the host views."""
+    frame = oracle.load_dat(os.path.join(PKTS, "QinQ_802.1_AD.dat"))
+    rec = oracle.parse_one(frame, flags=3)
+    eth = EtherFrame.parse(Packet(rec, frame)).unwrap()
+    assert eth.ethertype() == EtherType.QINQ
+    q = VlanFrame.parse(eth.payload()).unwrap()
+    assert q.vlan_id() == 30 and q.ethertype() == EtherType.VLAN
+    v = VlanFrame.parse(q.payload()).unwrap()
+    assert v.priority() == 0 and v.dei_flag() is False and v.vlan_id() == 100
+    assert v.ethertype() == EtherType.IPV4
+    assert Ipv4.parse(q.payload()).is_err()          # IPv4 is after the inner tag
+    ip = Ipv4.parse(v.payload()).unwrap()
+    assert ip.version() == 4 and ip.header_len() == 20 and ip.packet_len() == 1474
+    assert ip.ttl() == 255 and ip.protocol() == 253 and ip.checksum() == 0xddbf
+    assert len(ip.payload().chunk()) == 1454
+    assert ip.verify_checksum()
+
+
+def test_views_tcp_options():
+    """rpkt/tests/tcp_test.rs:17-43 through the host views."""
+    frame = oracle.load_dat(os.path.join(PKTS, "TcpPacketWithOptions.dat"))
+    rec = oracle.parse_one(frame, flags=3)
+    eth = EtherFrame.parse(Packet(rec, frame)).unwrap()
+    ip = Ipv4.parse(eth.payload()).unwrap()
+    tcp = Tcp.parse(ip.payload()).unwrap()
+    assert tcp.src_port() == 44147 and tcp.dst_port() == 80
+    assert tcp.seq_num() == 777047406 and tcp.ack_num() == 3761117865
+    assert tcp.header_len() - 20 == 12
+    assert (tcp.cwr(), tcp.ece(), tcp.urg(), tcp.ack(), tcp.psh(), tcp.rst(), tcp.syn(),
+            tcp.fin()) == (False, False, False, True, True, False, False, False)
+    assert tcp.window_size() == 913 and tcp.checksum() == 0xac20 and tcp.urgent_pointer() == 0
+    assert tcp.payload().cursor() == 14 + 20 + 32
+
+
+# ---- checksum.rs known answers -------------------------------------------------
+
+def test_from_slice_basic():
+    assert oracle.from_slice(b"") == 0
+    assert oracle.from_slice(b"\x00\x01") == 1
+    assert oracle.from_slice(b"\xff") == 0xff00            # odd tail << 8, checksum.rs:57-59
+    assert oracle.from_slice(b"\xff\xff\x00\x01") == 1     # end-around carry
+    assert oracle.from_slice(b"\x00\x00" * 40) == 0        # zero only for all-zero input
+    assert oracle.from_slice(b"\xff\xff" * 3) == 0xffff
+
+
+def test_from_buf_matches_from_slice_for_any_chunking():
+    rng = np.random.default_rng(7)
+    for trial in range(200):
+        n = int(rng.integers(0, 300))
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        cuts = sorted(set(int(c) for c in rng.integers(0, n + 1, int(rng.integers(0, 6)))))
+        segs, prev = [], 0
+        for c in cuts + [n]:
+            segs.append(data[prev:c])
+            prev = c
+        assert oracle.from_buf(segs) == oracle.from_slice(data), (trial, cuts)
+
+
+def test_combine_is_order_free_and_matches_concatenation():
+    rng = np.random.default_rng(8)
+    for _ in range(200):
+        a = rng.integers(0, 256, 2 * int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8).tobytes()
+        assert oracle.combine([oracle.from_slice(a), oracle.from_slice(b)]) == \
+            oracle.from_slice(a + b)
+
+
+def test_icmp_style_roundtrip():
+    """Stamping the complement of the sum makes the sum 0xffff (the KAT pattern of
+    rpkt/tests/icmpv4_test.rs:82-96)."""
+    rng = np.random.default_rng(9)
+    for _ in range(100):
+        n = 2 * int(rng.integers(2, 200))
+        data = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        data[2:4] = b"\x00\x00"
+        ck = (~oracle.from_slice(bytes(data))) & 0xffff
+        data[2:4] = bytes([ck >> 8, ck & 0xff])
+        assert oracle.from_slice(bytes(data)) == 0xffff
