@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident Ether/IPv4/{TCP,UDP} parse + checksum throughput.
+
+Metric (BASELINE.json): Mpps + GB/s device-resident parse+cksum, 64 B & 1500 B
+frames, 1/2/4/8 MI355X.  One "step" = one rpkt_gpu_parse_batch launch over one
+synthetic batch already resident in HBM.
+
+  headline  config 2: 1,048,576 x 64 B Ether/IPv4/UDP, stride 64, header extract +
+            IPv4 header sum.  Each rank rotates over 4 distinct batches so the
+            576 MiB working set is streamed from HBM, not the 256 MiB Infinity Cache.
+  also      config 3: 1,048,576 x 1500 B Ether/IPv4/TCP, full L3 + L4 sums
+            (reported under "extra").
+  --config 4: 8,388,608-frame IMIX sharded over the ranks (strong scaling) with
+            per-flow counters and one RCCL all-reduce of the counters.
+
+Multi-GPU: one process per GPU (torchrun); batches are independent, so ranks
+never exchange frames (weak scaling for configs 2/3).  The timed region is
+bracketed by barrier + synchronize and the max over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from rpkt_amd import engine, gen  # noqa: E402
+from rpkt_amd.records import REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
+
+METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FLAG_NAMES = {1: "ip_sum", 2: "l4_sum", 3: "ip_sum+l4_sum"}
+WORKLOAD = {2: "1M x 64B Ether/IPv4/UDP extract + IPv4 header checksum",
+            3: "1M x 1500B Ether/IPv4/TCP parse + full L3/L4 checksum",
+            4: "8M IMIX 64/570/1500 (7:4:1) TCP/UDP, sharded, flow counters + RCCL reduce",
+            5: "4M x U[64,1518]B 802.1Q/QinQ + IPv4 options -> TCP options"}
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, local, world
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def algorithmic_bytes(hb):
+    """Bytes one launch must move: every frame byte read + the 80-B record written
+    (+ 4 B offset per frame for the packed layout).  SURVEY.md §8d."""
+    b = int(hb.lens().sum()) + hb.n * REC_BYTES
+    if hb.offsets is not None:
+        b += 4 * (hb.n + 1)
+    return b
+
+
+def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
+    """Time `steps` launches (rotating over dbs).  Returns wall seconds (max over
+    ranks) and the mean per-launch kernel duration from HIP events recorded on the
+    launch stream around each launch."""
+    stream = torch.cuda.current_stream()
+    R = len(dbs)
+    nb = flow["n_buckets"] if flow else 0
+
+    def one(k):
+        db, rc = dbs[k % R], recs[k % R]
+        if flow:
+            engine.parse_batch(db, flags | F_FLOW_EV, recs=rc, flow_ev=flow["ev"][k % R],
+                               n_buckets=nb, stream=stream)
+            engine.flow_count(flow["ev"][k % R], db.n, nb, counters=flow["counters"],
+                              workspace=flow["ws"], stream=stream)
+        else:
+            engine.parse_batch(db, flags, recs=rc, stream=stream)
+
+    for k in range(warmup):
+        one(k)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev0[k].record(stream)
+        one(k)
+        ev1[k].record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    wall = max_over_ranks(t1 - t0, world)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev0, ev1)]))
+    return wall, kern_ms
+
+
+def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
+    """The CPU restatement of rpkt's path (oracle/, kind "port") timed on this host
+    over a bounded sample of the same workload; also checks the GPU records of the
+    sample bit-exact against it."""
+    from oracle import oracle
+    n = hb.n
+    t0 = time.perf_counter()
+    o = oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
+                           frame_len=hb.frame_len)
+    one = time.perf_counter() - t0
+    reps = max(1, int(seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
+                           frame_len=hb.frame_len)
+    dt = time.perf_counter() - t0
+    frames_total = n * reps
+    bytes_total = int(hb.lens().sum()) * reps
+    t0 = time.perf_counter()
+    oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
+                       frame_len=hb.frame_len, threads=threads_all)
+    dt_all = time.perf_counter() - t0
+    parity = gpu_recs.tobytes() == o.tobytes()
+    return {
+        "value": round(frames_total / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+        "gb_per_s": round(bytes_total / dt / 1e9, 3),
+        "sample": "%d reps x %d frames of the same batch, 1 thread, %.1f s" % (reps, n, dt),
+        "all_cores": {"threads": threads_all,
+                      "value": round(n / dt_all / 1e6, 3), "unit": "Mpps"},
+        "gpu_parity_on_sample": bool(parity),
+    }
+
+
+def run_config(cfg, args, rank, world, cpu=False):
+    flags = gen.FLAGS[cfg]
+    flow = None
+    if cfg == 4:                                   # strong scaling: shard one 8M batch
+        n_total = args.frames or gen.DEFAULT_N[4]
+        lo, hi = n_total * rank // world, n_total * (rank + 1) // world
+        hbs = [gen.make_batch(4, hi - lo, first=lo)]
+        scaling = "strong"
+    else:                                          # weak scaling: a batch per rank
+        n = args.frames or gen.DEFAULT_N[cfg]
+        R = args.rotate or (4 if cfg == 2 else 1)
+        hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
+               for r in range(R)]
+        scaling = "weak"
+    dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
+    recs = [engine.alloc_records(hb.n) for hb in hbs]
+    if cfg == 4:
+        nb = 8192
+        flow = {"n_buckets": nb,
+                "ev": [torch.empty(hb.n, dtype=torch.int64, device="cuda") for hb in hbs],
+                "counters": torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda"),
+                "ws": engine.flow_workspace(hbs[0].n, nb)}
+    torch.cuda.synchronize()
+    log(rank, "config %d: %d frames/rank x %d batches resident, flags=%d" % (
+        cfg, hbs[0].n, len(hbs), flags))
+    wall, kern_ms = time_parse(dbs, recs, flags, args.steps, args.warmup, world, flow)
+
+    frames_step = sum(hb.n for hb in hbs) / len(hbs)
+    bytes_step = sum(int(hb.lens().sum()) for hb in hbs) / len(hbs)
+    alg_step = sum(algorithmic_bytes(hb) for hb in hbs) / len(hbs)
+    mpps = frames_step * world * args.steps / wall / 1e6
+    gbps = bytes_step * world * args.steps / wall / 1e9
+    achieved = alg_step / (kern_ms / 1e3) / 1e9
+    out = {
+        "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
+        "kernel_ms": kern_ms, "scaling": scaling, "frames_per_rank": int(frames_step),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "alg_bytes_per_launch": int(alg_step)},
+        "flags": FLAG_NAMES[flags], "layout": ("stride%d" % hbs[0].stride) if hbs[0].stride
+        else "packed+u32 offsets",
+    }
+    if cfg == 4:
+        torch.cuda.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        if world > 1:
+            dist.all_reduce(flow["counters"], op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        red = time.perf_counter() - t0
+        c = flow["counters"].cpu().numpy().view(np.uint64).reshape(-1, 4)
+        steps_run = args.steps + args.warmup
+        out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
+        out["flow_pkts_total"] = int(c[:, 0].sum())
+        out["flow_pkts_expected"] = int(n_total * steps_run)
+    if cpu and rank == 0:
+        g = as_records(recs[0].cpu().numpy())
+        out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds, args.cpu_threads)
+    del dbs, recs
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--also", default="3", help="extra configs reported under 'extra'")
+    ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
+    ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank, local, world = dist_env()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    want_cpu = (not args.no_cpu) and world == 1
+
+    main_res = run_config(args.config, args, rank, world, cpu=want_cpu)
+    extra = {}
+    for c in [int(x) for x in args.also.split(",") if x.strip()]:
+        if c != args.config:
+            extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
+
+    if rank == 0:
+        fb = {2: 64, 3: 1500}.get(args.config)
+        line = {
+            "metric": METRIC,
+            "value": round(main_res["mpps"], 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(main_res["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": main_res["scaling"],
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded generator, rpkt-dpdk loopback_tx frame shapes)",
+            "config": {"workload": WORKLOAD[args.config], "frames_per_rank":
+                       main_res["frames_per_rank"], "frame_bytes": fb,
+                       "layout": main_res["layout"], "checksums": main_res["flags"],
+                       "parallelism": "replicas x%d (independent batches, no collective)" % world
+                       if args.config != 4 else "shard x%d + RCCL all-reduce" % world},
+            "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
+            "kernel_ms": round(main_res["kernel_ms"], 5),
+            "roofline": main_res["roofline"],
+            "cpu_baseline": main_res.get("cpu_baseline"),
+            "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                          for kk, vv in v.items()} for k, v in extra.items()},
+        }
+        for k in ("flow_reduce_ms", "flow_pkts_total", "flow_pkts_expected"):
+            if k in main_res:
+                line[k] = main_res[k]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,55 @@
+"""Build the native libraries in-tree (they travel to the GPU box with the repo).
+
+  rpkt_amd/_build/librpkt_gpu.so   HIP engine for gfx950 + C ABI (include/rpkt_gpu.h)
+  rpkt_amd/_build/librpkt_gen.so   host C++ synthetic frame generator
+
+hipcc cross-compiles gfx950 without a GPU.  Rebuilds only when a source is newer.
+"""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(HERE, "_build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("RPKT_OFFLOAD_ARCH", "gfx950")
+
+GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
+GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
+GPU_SRC = [os.path.join(HERE, "csrc", "rpkt_gpu.hip")]
+GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
+HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_gpu(force=False, extra=()):
+    os.makedirs(OUT, exist_ok=True)
+    if force or _stale(GPU_LIB, GPU_SRC + HDR):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-o", GPU_LIB] + list(extra) + GPU_SRC
+        subprocess.check_call(cmd)
+    return GPU_LIB
+
+
+def build_gen(force=False):
+    os.makedirs(OUT, exist_ok=True)
+    if force or _stale(GEN_LIB, GEN_SRC):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o", GEN_LIB] + \
+            GEN_SRC + ["-lpthread"]
+        subprocess.check_call(cmd)
+    return GEN_LIB
+
+
+def build_all(force=False):
+    return build_gpu(force), build_gen(force)
+
+
+if __name__ == "__main__":
+    import sys
+    print(build_all(force="--force" in sys.argv))

@@ -1,0 +1,319 @@
+// rpkt_gen.cpp — seeded synthetic frame generator (host C++), the loopback/
+// synthetic ingress that replaces rpkt-dpdk's NIC rx for the benchmark.
+//
+// Frames are built the way rpkt's build side does it — headers prepended onto a
+// payload with setters, checksums stamped last (benches/rpkt/rpkt_build.rs:9-28,
+// rpkt-dpdk/examples/loopback_tx.rs:70-99 for the UDP template, :52-68 for the
+// gen_ip_addrs flow spread) — with seeded fault injection on top (bad checksums,
+// truncation, bad IHL / data offset / lengths) so every parse status occurs.
+//
+// Every frame i is a pure function of (config, seed, i, len_i): generation is
+// parallel and reproducible.  The checksum arithmetic here is the product's own
+// build-side RFC 1071 code, independent of oracle/.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Rng {
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed) {}
+    uint64_t next() {  // splitmix64
+        uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    }
+    uint32_t below(uint32_t n) { return (uint32_t)((next() >> 32) * (uint64_t)n >> 32); }
+    bool chance(uint32_t per_10000) { return below(10000) < per_10000; }
+};
+
+inline void put16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+inline void put32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+// RFC 1071 one's-complement sum (big-endian words, odd tail << 8), folded.
+uint32_t ones_sum(const uint8_t* d, size_t n, uint32_t acc = 0) {
+    uint64_t a = acc;
+    size_t i = 0;
+    for (; i + 1 < n; i += 2) a += ((uint32_t)d[i] << 8) | d[i + 1];
+    if (i < n) a += (uint32_t)d[i] << 8;
+    while (a >> 16) a = (a & 0xffff) + (a >> 16);
+    return (uint32_t)a;
+}
+
+const uint8_t kDmac[6] = {0xac, 0xdc, 0xca, 0x79, 0xe5, 0xc6};  // loopback_tx.rs:38
+const uint8_t kSmac[6] = {0xac, 0xdc, 0xca, 0x79, 0xca, 0x86};  // loopback_tx.rs:39
+const uint32_t kDip = (192u << 24) | (168u << 16) | (23u << 8) | 2u;  // loopback_tx.rs:40
+
+// gen_ip_addrs(fst, snd, size)[k], loopback_tx.rs:52-68
+uint32_t gen_ip(uint32_t fst, uint32_t snd, uint32_t size, uint32_t k) {
+    k %= size;
+    uint32_t third, fourth;
+    if (k < (size / 250) * 250) { third = 2 + k / 250; fourth = 2 + k % 250; }
+    else { third = 2 + size / 250; fourth = 2 + (k - (size / 250) * 250); }
+    return (fst << 24) | (snd << 16) | (third << 8) | fourth;
+}
+
+struct Spec {
+    int nvlan = 0;
+    uint32_t tpid0 = 0x8100;
+    int ihl = 5;
+    bool tcp = false;
+    int doff = 5;
+    uint32_t src = 0, dst = kDip;
+    uint32_t sport = 60376, dport = 161;  // loopback_tx.rs:41-42
+    uint32_t ttl = 64, ident = 0;
+    int pad = 0;             // Ethernet padding bytes past IPv4 packet_len
+    bool bad_ip = false, bad_l4 = false, udp_zero = false;
+    bool rand_payload = false;
+    uint8_t payload_byte = 0xae;  // loopback_tx.rs:45
+    int fault = 0;           // 0 none; 1 truncate; 2 bad ihl; 3 tot>len; 4 bad udp len/doff; 5 tot<ihl; 6 not ipv4; 7 other proto; 8 short L4
+};
+
+// Option bytes for an IPv4 header of `bytes` option space (NOP / RecordRoute / EOL).
+void ipv4_options(uint8_t* o, int bytes, Rng& r) {
+    int i = 0;
+    while (i < bytes) {
+        int left = bytes - i;
+        uint32_t pick = r.below(3);
+        if (pick == 1 && left >= 7) {            // Record Route (type 7): len, ptr, slots
+            int slots = std::min((left - 3) / 4, 9);
+            int len = 3 + 4 * slots;
+            o[i] = 7; o[i + 1] = (uint8_t)len; o[i + 2] = 4;
+            for (int k = 3; k < len; k++) o[i + k] = (uint8_t)r.next();
+            i += len;
+        } else if (pick == 2) {                 // EOL, then zero fill
+            for (; i < bytes; i++) o[i] = 0;
+        } else {
+            o[i++] = 1;                          // NOP
+        }
+    }
+}
+
+// TCP options (NOP / MSS / WS / SACK-perm / TS) filling `bytes`.
+void tcp_options(uint8_t* o, int bytes, Rng& r) {
+    int i = 0;
+    while (i < bytes) {
+        int left = bytes - i;
+        uint32_t pick = r.below(5);
+        if (pick == 1 && left >= 4) { o[i] = 2; o[i + 1] = 4; put16(o + i + 2, 1460); i += 4; }
+        else if (pick == 2 && left >= 3) { o[i] = 3; o[i + 1] = 3; o[i + 2] = 7; i += 3; }
+        else if (pick == 3 && left >= 2) { o[i] = 4; o[i + 1] = 2; i += 2; }
+        else if (pick == 4 && left >= 10) {
+            o[i] = 8; o[i + 1] = 10; put32(o + i + 2, (uint32_t)r.next()); put32(o + i + 6, (uint32_t)r.next());
+            i += 10;
+        } else { o[i++] = 1; }
+    }
+}
+
+// Build one frame of exactly `len` bytes from spec into out.
+void build(const Spec& s, uint32_t len, uint8_t* out, Rng& r) {
+    static thread_local uint8_t scratch[(1u << 16) + 1024];
+    const uint32_t cap = std::min<uint32_t>(std::max<uint32_t>(len, 256) + 256, sizeof(scratch));
+    memset(scratch, 0, cap);
+    uint8_t* f = scratch;
+    memcpy(f, kDmac, 6);
+    memcpy(f + 6, kSmac, 6);
+    uint32_t off = 12;
+    if (s.nvlan >= 1) {
+        put16(f + off, s.tpid0); off += 2;
+        put16(f + off, (r.below(8) << 13) | (r.below(2) << 12) | r.below(4096)); off += 2;
+    }
+    if (s.nvlan >= 2) {
+        put16(f + off, 0x8100); off += 2;
+        put16(f + off, (r.below(8) << 13) | (r.below(2) << 12) | r.below(4096)); off += 2;
+    }
+    put16(f + off, s.fault == 6 ? 0x86dd : 0x0800); off += 2;
+    const uint32_t l3 = off;
+    const uint32_t ihl4 = (uint32_t)s.ihl * 4;
+    const uint32_t l4h = s.tcp ? (uint32_t)s.doff * 4 : 8;
+    // IPv4 packet_len fills the frame minus padding (never below the headers).
+    int64_t tot = (int64_t)len - l3 - s.pad;
+    if (tot < (int64_t)(ihl4 + l4h)) tot = ihl4 + l4h;
+    const uint32_t l4 = l3 + ihl4;
+    const uint32_t l4len = (uint32_t)tot - ihl4;
+    // payload
+    uint8_t* pl = f + l4 + l4h;
+    int64_t pln = (int64_t)l4len - l4h;
+    for (int64_t k = 0; k < pln; k++) pl[k] = s.rand_payload ? (uint8_t)r.next() : s.payload_byte;
+    // L4 header (rpkt_build.rs:13-16 / loopback_tx.rs:73-77 for UDP)
+    uint8_t* h4 = f + l4;
+    put16(h4, s.sport);
+    put16(h4 + 2, s.dport);
+    if (s.tcp) {
+        put32(h4 + 4, (uint32_t)r.next());
+        put32(h4 + 8, (uint32_t)r.next());
+        uint32_t flags = 0x10 | (r.below(2) << 3);
+        put16(h4 + 12, ((uint32_t)s.doff << 12) | flags);
+        put16(h4 + 14, 1024 + r.below(60000));
+        put16(h4 + 16, 0);
+        put16(h4 + 18, 0);
+        tcp_options(h4 + 20, (int)l4h - 20, r);
+    } else {
+        put16(h4 + 4, l4len);
+        put16(h4 + 6, 0);
+    }
+    // IPv4 header (rpkt_build.rs:18-22)
+    uint8_t* ip = f + l3;
+    ip[0] = (uint8_t)(0x40 | s.ihl);
+    ip[1] = 0;
+    put16(ip + 2, (uint32_t)tot);
+    put16(ip + 4, s.ident);
+    put16(ip + 6, 0x4000);
+    ip[8] = (uint8_t)s.ttl;
+    ip[9] = s.tcp ? 6 : 17;
+    put16(ip + 10, 0);
+    put32(ip + 12, s.src);
+    put32(ip + 16, s.dst);
+    ipv4_options(ip + 20, (int)ihl4 - 20, r);
+    // checksums: L4 over pseudo header + segment, then IPv4 header
+    uint32_t ps = (s.src >> 16) + (s.src & 0xffff) + (s.dst >> 16) + (s.dst & 0xffff) +
+                  (s.tcp ? 6u : 17u) + l4len;
+    uint32_t ck = (~ones_sum(h4, l4len, ps)) & 0xffff;
+    if (!s.tcp && ck == 0) ck = 0xffff;                     // RFC 768
+    if (s.bad_l4) { ck ^= 0x5a5a; if (ck == 0) ck = 1; }
+    if (!s.tcp && s.udp_zero) ck = 0;
+    put16(h4 + (s.tcp ? 16 : 6), ck);
+    uint32_t ick = (~ones_sum(ip, ihl4)) & 0xffff;
+    if (s.bad_ip) ick ^= 0x00ff;
+    put16(ip + 10, ick);
+    // structural faults (after checksums: the frame is then malformed on purpose)
+    switch (s.fault) {
+        case 2: ip[0] = (uint8_t)(0x40 | r.below(5)); break;                 // ihl < 5
+        case 3: put16(ip + 2, (uint32_t)tot + 1 + r.below(64)); break;       // tot > remaining
+        case 4:
+            if (s.tcp) h4[12] = (uint8_t)((r.below(5)) << 4);                // doff < 5
+            else put16(h4 + 4, r.chance(5000) ? r.below(8) : l4len + 1 + r.below(16));
+            break;
+        case 5: put16(ip + 2, r.below(ihl4)); break;                          // tot < ihl
+        case 7: { uint32_t p = r.below(256); ip[9] = (uint8_t)((p == 6 || p == 17) ? 47 : p); break; }
+        case 8: put16(ip + 2, ihl4 + r.below(s.tcp ? 20 : 8)); break;          // L4 too short
+        default: break;
+    }
+    memcpy(out, f, len);
+}
+
+// config: 1 bench_rpkt (1k x 64B UDP, rpkt_build.rs header values), 2 64B UDP,
+// 3 1500B TCP, 4 IMIX mixed, 5 VLAN/QinQ + options TCP, 6 fuzz (all statuses).
+Spec spec_for(int config, uint64_t seed, uint32_t i, uint32_t len, Rng& r) {
+    Spec s;
+    switch (config) {
+        case 1:  // benches/rpkt/rpkt_build.rs:13-27
+            s.src = (192u << 24) | (168u << 16) | (29u << 8) | 58u;
+            s.dst = (192u << 24) | (168u << 16) | (29u << 8) | 160u;
+            s.ttl = 128; s.ident = 0x5c65;
+            break;
+        case 2:
+            s.src = gen_ip(172, 74, 8192, i);
+            s.bad_ip = r.chance(100);
+            s.ttl = 64; s.ident = i & 0xffff;
+            break;
+        case 3:
+            s.tcp = true; s.src = gen_ip(172, 74, 8192, i); s.rand_payload = true;
+            s.sport = 1024 + r.below(60000); s.dport = 80;
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            s.ident = i & 0xffff;
+            break;
+        case 4:
+            s.tcp = r.below(2) == 1; s.src = gen_ip(172, 74, 8192, r.below(8192));
+            s.sport = 1024 + r.below(4096); s.dport = s.tcp ? 80 : 53;
+            s.rand_payload = true;
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            s.ident = i & 0xffff;
+            break;
+        case 5:
+            s.nvlan = r.below(2) ? 2 : 1;
+            s.tpid0 = s.nvlan == 2 ? 0x88a8 : 0x8100;
+            s.ihl = 5 + (int)r.below(11);
+            s.tcp = true; s.doff = 5 + (int)r.below(11);
+            s.src = gen_ip(172, 74, 8192, r.below(8192)); s.sport = 1024 + r.below(60000);
+            s.dport = 443; s.rand_payload = true;
+            s.pad = r.chance(1000) ? (int)r.below(9) : 0;
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            break;
+        default: {  // 6: fuzz — every status, odd alignments, tiny frames
+            s.nvlan = (int)r.below(4) == 0 ? (int)r.below(3) : 0;
+            s.tpid0 = r.below(2) ? 0x88a8 : 0x8100;
+            s.ihl = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            s.tcp = r.below(2) == 1;
+            s.doff = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            s.src = (uint32_t)r.next(); s.dst = (uint32_t)r.next();
+            s.sport = r.below(65536); s.dport = r.below(65536);
+            s.rand_payload = true;
+            s.pad = r.below(8) == 0 ? (int)r.below(12) : 0;
+            s.bad_ip = r.chance(1000); s.bad_l4 = r.chance(1000);
+            s.udp_zero = r.chance(500);
+            s.fault = r.below(4) == 0 ? 1 + (int)r.below(8) : 0;
+            break;
+        }
+    }
+    (void)seed; (void)len;
+    return s;
+}
+
+void fill_range(int config, uint64_t seed, uint64_t first, const uint32_t* offsets,
+                const uint32_t* lens, uint32_t stride, uint32_t lo, uint32_t hi, uint8_t* frames) {
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint64_t gi = first + i;                    // global frame index
+        Rng r(seed * 0x100000001b3ull ^ (0x9e3779b97f4a7c15ull * (gi + 1)));
+        uint32_t len = lens[i];
+        uint64_t off = offsets ? offsets[i] : (uint64_t)i * stride;
+        Spec s = spec_for(config, seed, (uint32_t)gi, len, r);
+        if (config == 6 && s.fault == 1) {
+            // truncation: build a full frame then cut it at a random length
+            uint32_t full = len + 64;
+            std::vector<uint8_t> tmp(full);
+            Spec s2 = s;
+            s2.fault = 0;
+            build(s2, full, tmp.data(), r);
+            memcpy(frames + off, tmp.data(), len);
+        } else {
+            build(s, len, frames + off, r);
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Frame lengths for a config (IMIX 64/570/1500 at 7:4:1; config 5 U[64,1518];
+// fuzz U[0,300] with a 1500-B tail).  Deterministic in (config, seed, i).
+void rpkt_gen_lengths(int config, uint64_t seed, uint64_t first, uint32_t n, uint32_t* lens) {
+    for (uint32_t i = 0; i < n; i++) {
+        Rng r(seed * 0x2545f4914f6cdd1dull ^ (0xd1b54a32d192ed03ull * (first + i + 1)));
+        uint32_t L;
+        switch (config) {
+            case 1: case 2: L = 64; break;
+            case 3: L = 1500; break;
+            case 4: { uint32_t k = r.below(12); L = k < 7 ? 64 : (k < 11 ? 570 : 1500); break; }
+            case 5: L = 64 + r.below(1518 - 64 + 1); break;
+            default: L = r.below(8) == 0 ? 1000 + r.below(600) : r.below(301); break;
+        }
+        lens[i] = L;
+    }
+}
+
+// Fill frames [first, first + n) of the global sequence.  Packed layout: offsets
+// (n+1 entries, relative to `frames`) given; strided: offsets NULL.
+int rpkt_gen_fill(int config, uint64_t seed, uint64_t first, uint32_t n, const uint32_t* lens,
+                  const uint32_t* offsets, uint32_t stride, uint8_t* frames, int threads) {
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n / 1024 + 1) threads = (int)(n / 1024 + 1);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        uint32_t lo = (uint32_t)((uint64_t)n * t / threads);
+        uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+        th.emplace_back(fill_range, config, seed, first, offsets, lens, stride, lo, hi, frames);
+    }
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+}  // extern "C"

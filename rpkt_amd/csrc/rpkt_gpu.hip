@@ -1,0 +1,643 @@
+// rpkt_gpu.hip — MI355X (gfx950, CDNA4) batch engine for rpkt's
+// Ether -> (802.1Q/802.1ad)* -> IPv4 -> {TCP, UDP} decode-and-verify path.
+//
+// One wavefront owns a tile of 64 frames.  The work is split three ways:
+//   1. header window: the wave copies the first 128 aligned bytes of each of
+//      its 64 frames into LDS with 16-byte buffer loads (8 chunks per frame,
+//      one 1 KiB contiguous LDS write per wave-instruction);
+//   2. lane-per-frame parse from LDS: the rpkt parse chain (EtherFrame::parse
+//      ether/generated.rs:34-41, VlanFrame::parse vlan/generated.rs:32-39,
+//      Ipv4::parse ipv4/generated.rs:35-51, Udp::parse udp/generated.rs:31-42,
+//      Tcp::parse tcp/generated.rs:34-45) with every getter into registers, the
+//      IPv4 header sum and the in-window part of the L4 sum;
+//   3. the rest of each L4 segment (frames longer than the window) as ONE
+//      flattened stream of 16-byte chunks over the whole tile: consecutive lanes
+//      read consecutive chunks (coalesced HBM reads whatever the frame sizes),
+//      each chunk's masked word sum enters a wave prefix scan (DPP), and every
+//      frame's sum is the scan difference between its last and first chunk.
+// All partial sums are taken over absolute-address-aligned little-endian
+// 16-bit words; RFC 1071 byte-order independence makes the big-endian sum of a
+// range equal to that sum when the range starts at an odd address and to its
+// byte swap when it starts at an even one (checksum.rs:33-62 semantics,
+// including the odd tail byte << 8 of :57-59).
+//
+// Loads go through a buffer resource descriptor whose range is frames_bytes, so
+// a malformed offset table can only produce wrong records, never a fault.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/rpkt_gpu.h"
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;            // lanes per wavefront (CDNA)
+constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
+constexpr int kWin = 128;            // header window bytes per frame in LDS
+constexpr int kWinChunks = kWin / 16;
+constexpr int kStreamUnroll = 4;     // 16-B chunk loads in flight per lane per step
+constexpr uint64_t kMaxFrameBytes = 0xffffff00ull;  // voffset + 16 never wraps
+
+struct WaveScratch {
+    uint8_t  win[kWave * kWin];      // 8 KiB header windows
+    uint32_t fo[kWave];              // frame offsets
+    uint32_t fl[kWave];              // frame lengths
+    uint32_t pref[kWave + 1];        // stream: exclusive prefix of chunk counts
+    uint32_t s[kWave];               // stream: range start (absolute byte)
+    uint32_t e[kWave];               // stream: range end (absolute byte)
+    uint32_t first[kWave];           // stream: scan value before a range's first chunk
+    uint32_t last[kWave];            // stream: scan value at a range's last chunk
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                             0x00020000);
+}
+
+__device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+}
+
+// Inclusive prefix sum over the 64 lanes (DPP: row shifts then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// propagate_carries (checksum.rs:115-118) for any u32 partial: 0 iff x == 0.
+__device__ __forceinline__ uint32_t fold16(uint32_t x) {
+    x = (x & 0xffffu) + (x >> 16);
+    x = (x & 0xffffu) + (x >> 16);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) {
+    return ((x & 0xffu) << 8) | (x >> 8);
+}
+
+// Big-endian RFC 1071 sum of a range from its absolute-phase LE partial.
+__device__ __forceinline__ uint32_t be_sum(uint32_t le_partial, uint32_t start_abs) {
+    uint32_t f = fold16(le_partial);
+    return (start_abs & 1u) ? f : bswap16(f);
+}
+
+// Keep bytes [lo, hi) of a little-endian dword (lo, hi clamped to 0..4).
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    hi = hi < 0 ? 0 : (hi > 4 ? 4 : hi);
+    uint32_t mh = (uint32_t)((1ull << (8 * hi)) - 1);
+    uint32_t ml = (uint32_t)((1ull << (8 * lo)) - 1);
+    return mh & ~ml;
+}
+
+__device__ __forceinline__ uint32_t halves(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+
+// Word sum of bytes [lo, hi) of a 16-byte chunk (absolute phase).
+__device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
+    if (lo <= 0 && hi >= 16) return halves(d.x) + halves(d.y) + halves(d.z) + halves(d.w);
+    return halves(d.x & byte_mask(lo, hi)) + halves(d.y & byte_mask(lo - 4, hi - 4)) +
+           halves(d.z & byte_mask(lo - 8, hi - 8)) + halves(d.w & byte_mask(lo - 12, hi - 12));
+}
+
+// Word sum of LDS bytes [s, e) (LDS byte addresses with the frame's absolute phase).
+__device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* lds, uint32_t s, uint32_t e) {
+    uint32_t acc = 0;
+    for (uint32_t a = s & ~3u; a < e; a += 4) {
+        uint32_t w = *reinterpret_cast<const uint32_t*>(lds + a);
+        w &= byte_mask((int)s - (int)a, (int)e - (int)a);
+        acc += halves(w);
+    }
+    return acc;
+}
+
+// Flattened chunk stream over the tile: lane q owns absolute byte range
+// [s_abs, e_abs) (empty allowed); returns that range's absolute-phase word sum.
+// Consecutive lanes read consecutive 16-byte chunks of the concatenated ranges.
+// `oob` is the descriptor's byte range: a voffset there loads zeros, no traffic.
+__device__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob, uint32_t s_abs,
+                                    uint32_t e_abs, WaveScratch& W, int lane) {
+    uint32_t nch = e_abs > s_abs ? ((e_abs - 1) >> 4) - (s_abs >> 4) + 1 : 0;
+    uint32_t incl = wave_incl_scan(nch);
+    uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    if (total == 0) return 0;                                    // wave-uniform
+    W.pref[lane] = incl - nch;
+    if (lane == 63) W.pref[64] = incl;
+    W.s[lane] = s_abs;
+    W.e[lane] = e_abs;
+    W.first[lane] = 0;
+    W.last[lane] = 0;
+    wave_sync();
+
+    uint32_t run = 0;                                            // scan carry (uniform)
+    for (uint32_t base = 0; base < total; base += kWave * kStreamUnroll) {
+        u32x4 d[kStreamUnroll];
+        uint32_t q[kStreamUnroll], a[kStreamUnroll];
+#pragma unroll
+        for (int u = 0; u < kStreamUnroll; ++u) {
+            uint32_t c = base + u * kWave + lane;
+            uint32_t lo = 0;
+#pragma unroll
+            for (int step = 32; step; step >>= 1)
+                if (W.pref[lo + step] <= c) lo += step;
+            q[u] = lo;
+            a[u] = ((W.s[lo] & ~15u) + 16u * (c - W.pref[lo]));
+            d[u] = load16(rs, c < total ? a[u] : oob);
+        }
+#pragma unroll
+        for (int u = 0; u < kStreamUnroll; ++u) {
+            uint32_t c = base + u * kWave + lane;
+            uint32_t v = 0;
+            if (c < total) {
+                int lo = (int)W.s[q[u]] - (int)a[u];
+                int hi = (int)W.e[q[u]] - (int)a[u];
+                v = chunk_sum(d[u], lo, hi);
+            }
+            uint32_t sc = wave_incl_scan(v) + run;
+            run = __builtin_amdgcn_readlane(sc, 63);
+            if (c < total) {
+                if (c == W.pref[q[u]]) W.first[q[u]] = sc - v;
+                if (c + 1 == W.pref[q[u] + 1]) W.last[q[u]] = sc;
+            }
+        }
+    }
+    wave_sync();
+    return nch ? W.last[lane] - W.first[lane] : 0;
+}
+
+struct Frame { uint32_t off, len; };
+
+__device__ __forceinline__ Frame frame_span(const uint32_t* offsets, uint32_t stride,
+                                            uint32_t frame_len, uint32_t frames_bytes,
+                                            uint32_t i) {
+    uint64_t off, len;
+    if (offsets) {
+        uint32_t a = offsets[i], b = offsets[i + 1];
+        off = a;
+        len = b >= a ? b - a : 0;
+    } else {
+        off = (uint64_t)i * stride;
+        len = frame_len;
+    }
+    if (off > frames_bytes) off = frames_bytes;
+    if (off + len > frames_bytes) len = frames_bytes - off;
+    return Frame{(uint32_t)off, (uint32_t)len};
+}
+
+__device__ __forceinline__ uint32_t flow_hash(uint32_t src, uint32_t dst, uint32_t sp,
+                                              uint32_t dp, uint32_t proto) {
+    uint32_t h = 0x811c9dc5u;
+    h = (h ^ src) * 0x01000193u;
+    h = (h ^ dst) * 0x01000193u;
+    h = (h ^ ((sp << 16) | dp)) * 0x01000193u;
+    h = (h ^ proto) * 0x01000193u;
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                  const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                  uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
+                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+
+    Frame fr = {0, 0};
+    if (valid) fr = frame_span(offsets, stride, frame_len, frames_bytes, i);
+    W.fo[lane] = fr.off;
+    W.fl[lane] = fr.len;
+    wave_sync();
+
+    // ---- 1. header windows -> LDS (chunk c = frame c/8, piece c%8) ----
+    {
+        u32x4 d[kWinChunks];
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) {
+            const uint32_t c = k * kWave + lane;
+            const uint32_t q = c / kWinChunks, j = c % kWinChunks;
+            const uint32_t qo = W.fo[q], ql = W.fl[q];
+            const uint32_t a = (qo & ~15u) + 16u * j;
+            d[k] = load16(rs, (a < qo + ql) ? a : frames_bytes);
+        }
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k)
+            *reinterpret_cast<u32x4*>(&W.win[(k * kWave + lane) * 16]) = d[k];
+    }
+    wave_sync();
+
+    // ---- 2. lane-per-frame parse from LDS ----
+    const uint32_t ph = fr.off & 15u;                  // frame byte x at win[ph + x]
+    const uint8_t* wb = &W.win[lane * kWin];
+    const uint8_t* f = wb + ph;
+    auto b8 = [&](uint32_t o) -> uint32_t { return f[o]; };
+    auto be16 = [&](uint32_t o) -> uint32_t { return (b8(o) << 8) | b8(o + 1); };
+    auto le32 = [&](uint32_t o) -> uint32_t {
+        return b8(o) | (b8(o + 1) << 8) | (b8(o + 2) << 16) | (b8(o + 3) << 24);
+    };
+    auto be32 = [&](uint32_t o) -> uint32_t {
+        return (b8(o) << 24) | (b8(o + 1) << 16) | (b8(o + 2) << 8) | b8(o + 3);
+    };
+
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    uint32_t status = RPKT_S_OK, nvlan = 0;
+    const uint32_t len = fr.len;
+    uint32_t stream_s = 0, stream_e = 0;             // absolute L4 bytes past the window
+    uint32_t l4_part = 0, l4_start_abs = 0, pseudo = 0;
+    bool want_l4 = false;
+    w[19] = len;
+
+    if (!valid) {
+        status = RPKT_S_ETH_SHORT;
+    } else if (len < 14) {                             // ether/generated.rs:36
+        status = RPKT_S_ETH_SHORT;
+    } else {
+        uint32_t et = be16(12);                         // ether/generated.rs:55-59
+        w[1] = le32(0);
+        w[2] = b8(4) | (b8(5) << 8) | (b8(6) << 16) | (b8(7) << 24);
+        w[3] = le32(8);
+        uint32_t cur = 14, rem = len - 14;              // payload(), :63-67
+        uint32_t tci0 = 0, tci1 = 0, vet0 = 0, vet1 = 0;
+        while ((et == 0x8100u || et == 0x88a8u) && nvlan < RPKT_MAX_VLAN) {
+            if (rem < 4) { status = RPKT_S_VLAN_SHORT; break; }   // vlan/generated.rs:34
+            uint32_t tci = be16(cur);
+            et = be16(cur + 2);
+            if (nvlan == 0) { tci0 = tci; vet0 = et; } else { tci1 = tci; vet1 = et; }
+            nvlan++;
+            cur += 4;
+            rem -= 4;
+        }
+        w[4] = tci0 | (tci1 << 16);
+        w[5] = vet0 | (vet1 << 16);
+        uint32_t eth_et = be16(12);
+        if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+        if (status == RPKT_S_OK) {
+            // Ipv4::parse, ipv4/generated.rs:35-51
+            w[16] = cur;                                       // l3_off
+            if (rem < 20) {
+                status = RPKT_S_IP_SHORT;
+            } else {
+                const uint32_t b0 = b8(cur);
+                const uint32_t ihl4 = (b0 & 0xfu) * 4u;
+                const uint32_t tot = be16(cur + 2);
+                if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
+                else if (ihl4 > rem) status = RPKT_S_IP_IHL_GT_LEN;
+                else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
+                else if (tot > rem) status = RPKT_S_IP_TOT_GT_LEN;
+                if (status == RPKT_S_OK) {
+                    const uint32_t proto = b8(cur + 9);
+                    const uint32_t src = be32(cur + 12), dst = be32(cur + 16);
+                    w[6] = b0 | (b8(cur + 1) << 8) | (tot << 16);
+                    w[7] = be16(cur + 4) | (be16(cur + 6) << 16);
+                    w[8] = b8(cur + 8) | (proto << 8) | (be16(cur + 10) << 16);
+                    w[9] = src;
+                    w[10] = dst;
+                    uint32_t ip_sum = 0;
+                    if (flags & RPKT_F_IP_SUM)
+                        ip_sum = be_sum(lds_range_sum(wb, ph + cur, ph + cur + ihl4),
+                                        fr.off + cur);
+                    const uint32_t l4 = cur + ihl4;            // Ipv4::payload, :115-127
+                    const uint32_t l4rem = tot - ihl4;
+                    w[16] |= l4 << 16;
+                    w[17] = l4 | (l4rem << 16);
+                    w[18] = ip_sum;
+                    uint32_t l4len = 0;
+                    if (proto == 17u) {
+                        // Udp::parse, udp/generated.rs:31-42
+                        if (l4rem < 8) status = RPKT_S_UDP_SHORT;
+                        else {
+                            const uint32_t ulen = be16(l4 + 4);
+                            if (ulen < 8 || ulen > l4rem) status = RPKT_S_UDP_BAD_LEN;
+                            else {
+                                w[11] = be16(l4) | (be16(l4 + 2) << 16);
+                                w[14] = ulen;
+                                w[15] = be16(l4 + 6);
+                                w[17] = (l4 + 8) | ((ulen - 8) << 16);   // Udp::payload :66-76
+                                l4len = ulen;
+                            }
+                        }
+                    } else if (proto == 6u) {
+                        // Tcp::parse, tcp/generated.rs:34-45
+                        if (l4rem < 20) status = RPKT_S_TCP_SHORT;
+                        else {
+                            const uint32_t hl = (b8(l4 + 12) >> 4) * 4u;
+                            if (hl < 20 || hl > l4rem) status = RPKT_S_TCP_BAD_DOFF;
+                            else {
+                                w[11] = be16(l4) | (be16(l4 + 2) << 16);
+                                w[12] = be32(l4 + 4);
+                                w[13] = be32(l4 + 8);
+                                w[14] = be16(l4 + 12) | (be16(l4 + 14) << 16);
+                                w[15] = be16(l4 + 16) | (be16(l4 + 18) << 16);
+                                w[17] = (l4 + hl) | ((l4rem - hl) << 16);  // Tcp::payload
+                                l4len = l4rem;
+                            }
+                        }
+                    } else {
+                        status = RPKT_S_L4_OTHER;
+                    }
+                    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+                        want_l4 = true;
+                        // pseudo header (smoltcp pseudo_header_v4): src, dst, proto, len
+                        pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) +
+                                 proto + l4len;
+                        const uint32_t win_end = kWin - ph;   // frame offset where LDS ends
+                        const uint32_t e = l4 + l4len;
+                        const uint32_t e_in = e < win_end ? e : win_end;
+                        l4_part = lds_range_sum(wb, ph + l4, ph + e_in);
+                        l4_start_abs = fr.off + l4;
+                        if (e > win_end) {
+                            stream_s = fr.off + win_end;
+                            stream_e = fr.off + e;
+                        }
+                    }
+                }
+            }
+        }
+        w[0] = status | (nvlan << 8) | (eth_et << 16);
+    }
+    if (!valid || len < 14) w[0] = status;
+
+    // ---- 3. flattened stream for L4 bytes beyond the window (uniform call) ----
+    if (flags & RPKT_F_L4_SUM) {
+        uint32_t sp = wave_stream_sum(rs, frames_bytes, stream_s, stream_e, W, lane);
+        if (want_l4) {
+            const uint32_t seg = be_sum(l4_part + sp, l4_start_abs);
+            w[18] |= fold16(pseudo + seg) << 16;
+        }
+    }
+
+    if (valid) {
+        u32x4* out = reinterpret_cast<u32x4*>(recs + i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            out[k] = u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+        if (flags & RPKT_F_FLOW_EV) {
+            uint64_t ev = len;
+            uint32_t bucket = n_buckets;
+            const uint32_t proto = (w[8] >> 8) & 0xffu;
+            const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
+            if (status == RPKT_S_OK)
+                bucket = flow_hash(w[9], w[10], w[11] & 0xffffu, w[11] >> 16, proto) % n_buckets;
+            ev |= (uint64_t)bucket << 32;
+            if (ip_parsed && (w[18] & 0xffffu) != 0xffffu) ev |= 1ull << 48;
+            if (status == RPKT_S_OK && (w[18] >> 16) != 0xffffu &&
+                !(proto == 17u && (w[15] & 0xffffu) == 0))
+                ev |= 1ull << 49;
+            flow_ev[i] = ev;
+        }
+    }
+}
+
+// ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
+// One workgroup per CU-sized slice of the events; each keeps {pkts, bytes,
+// ip_bad | l4_bad << 16} per bucket in LDS (u32; a slice holds < 65536 events,
+// so no field can overflow), writes it once to its slab, and a second kernel
+// sums the slabs in a fixed order (bitwise reproducible counters).
+constexpr int kFlowThreads = 512;
+constexpr uint32_t kFlowLdsMax = 8192;      // buckets (+1 unparsed row) privatised in LDS
+constexpr uint32_t kFlowMaxPerBlock = 32768;
+constexpr uint32_t kFlowMinBlocks = 256;
+constexpr int kFlowUnroll = 8;
+
+__host__ __device__ inline uint32_t flow_blocks(uint32_t n) {
+    uint32_t b = (n + kFlowMaxPerBlock - 1) / kFlowMaxPerBlock;
+    uint32_t m = (n + kFlowThreads - 1) / kFlowThreads;   // >= one event per thread
+    uint32_t want = kFlowMinBlocks < m ? kFlowMinBlocks : m;
+    return b > want ? b : (want ? want : 1);
+}
+
+__global__ __launch_bounds__(kFlowThreads)
+void flow_hist_kernel(const uint64_t* __restrict__ ev, uint32_t n, uint32_t per_block,
+                      uint32_t n_buckets, uint32_t* __restrict__ slab) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];   // 3 * (n_buckets + 1)
+    const uint32_t rows = n_buckets + 1;
+    for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) h[r] = 0;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * per_block;
+    const uint32_t hi = min(n, lo + per_block);
+    for (uint32_t i0 = lo; i0 < hi; i0 += kFlowThreads * kFlowUnroll) {
+        uint64_t e[kFlowUnroll];
+#pragma unroll
+        for (int u = 0; u < kFlowUnroll; ++u) {
+            const uint32_t i = i0 + u * kFlowThreads + threadIdx.x;
+            e[u] = i < hi ? ev[i] : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kFlowUnroll; ++u) {
+            if (e[u] == ~0ull) continue;
+            uint32_t b = (uint32_t)(e[u] >> 32) & 0xffffu;
+            if (b > n_buckets) b = n_buckets;
+            atomicAdd(&h[b], 1u);
+            atomicAdd(&h[rows + b], (uint32_t)e[u]);
+            const uint32_t bad =
+                (uint32_t)((e[u] >> 48) & 1u) | ((uint32_t)((e[u] >> 49) & 1u) << 16);
+            if (bad) atomicAdd(&h[2 * rows + b], bad);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = slab + (size_t)blockIdx.x * 3 * rows;
+    for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) out[r] = h[r];
+}
+
+__global__ void flow_reduce_kernel(const uint32_t* __restrict__ slab, uint32_t n_slabs,
+                                   uint32_t n_buckets, uint64_t* __restrict__ counters) {
+    const uint32_t rows = n_buckets + 1;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= rows) return;
+    uint64_t pk = 0, by = 0, ipb = 0, l4b = 0;
+    for (uint32_t s = 0; s < n_slabs; ++s) {
+        const uint32_t* sl = slab + (size_t)s * 3 * rows;
+        pk += sl[b];
+        by += sl[rows + b];
+        const uint32_t bad = sl[2 * rows + b];
+        ipb += bad & 0xffffu;
+        l4b += bad >> 16;
+    }
+    counters[4 * b + 0] += pk;
+    counters[4 * b + 1] += by;
+    counters[4 * b + 2] += ipb;
+    counters[4 * b + 3] += l4b;
+}
+
+// n_buckets above the LDS limit: one global atomic set per event.
+__global__ void flow_atomic_kernel(const uint64_t* __restrict__ ev, uint32_t n,
+                                   uint32_t n_buckets, unsigned long long* counters) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t e = ev[i];
+        uint32_t b = (uint32_t)(e >> 32) & 0xffffu;
+        if (b > n_buckets) b = n_buckets;
+        atomicAdd(&counters[4 * b + 0], 1ull);
+        atomicAdd(&counters[4 * b + 1], (unsigned long long)(e & 0xffffffffu));
+        if ((e >> 48) & 1u) atomicAdd(&counters[4 * b + 2], 1ull);
+        if ((e >> 49) & 1u) atomicAdd(&counters[4 * b + 3], 1ull);
+    }
+}
+
+// ---- batched checksum::from_slice over ranges ----
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void checksum_ranges_kernel(const uint8_t* __restrict__ buf, uint32_t buf_bytes,
+                            const uint32_t* __restrict__ ranges, uint32_t n,
+                            uint16_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    uint32_t s = 0, e = 0;
+    if (i < n) {
+        uint64_t st = ranges[2 * i], ln = ranges[2 * i + 1];
+        if (st > buf_bytes) st = buf_bytes;
+        if (st + ln > buf_bytes) ln = buf_bytes - st;
+        s = (uint32_t)st;
+        e = (uint32_t)(st + ln);
+    }
+    const uint32_t part =
+        wave_stream_sum(make_rsrc(buf, buf_bytes), buf_bytes, s, e, scratch[wid], lane);
+    if (i < n) out[i] = (uint16_t)be_sum(part, s);
+}
+
+thread_local int g_last_hip_error = 0;
+
+inline int hip_check(hipError_t e) {
+    if (e != hipSuccess) {
+        g_last_hip_error = (int)e;
+        return RPKT_E_HIP;
+    }
+    return RPKT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rpkt_gpu_abi_version(void) { return RPKT_ABI_VERSION; }
+
+const char* rpkt_gpu_build_info(void) {
+    return "rpkt_gpu " __DATE__ " gfx950 hip; rec=80B; tile=64 frames/wave; win=128B";
+}
+
+const char* rpkt_gpu_status_name(int s) {
+    static const char* names[] = {"OK", "ETH_SHORT", "VLAN_SHORT", "NOT_IPV4", "IP_SHORT",
+                                  "IP_BAD_IHL", "IP_IHL_GT_LEN", "IP_TOT_LT_IHL",
+                                  "IP_TOT_GT_LEN", "L4_OTHER", "UDP_SHORT", "UDP_BAD_LEN",
+                                  "TCP_SHORT", "TCP_BAD_DOFF"};
+    return (s >= 0 && s < (int)(sizeof(names) / sizeof(names[0]))) ? names[s] : "?";
+}
+
+int rpkt_gpu_last_hip_error(void) { return g_last_hip_error; }
+
+uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_t dp,
+                        uint8_t proto) {
+    uint32_t h = 0x811c9dc5u;
+    h = (h ^ ip_src) * 0x01000193u;
+    h = (h ^ ip_dst) * 0x01000193u;
+    h = (h ^ (((uint32_t)sp << 16) | dp)) * 0x01000193u;
+    h = (h ^ proto) * 0x01000193u;
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+
+int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs_dev,
+                         rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    hipLaunchKernelGGL(parse_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                       b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen,
+                       b->n, flags, recs_dev, flow_ev_dev, n_buckets);
+    return hip_check(hipGetLastError());
+}
+
+size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets) {
+    if (n_buckets > kFlowLdsMax) return 16;
+    return (size_t)flow_blocks(n) * 3 * (size_t)(n_buckets + 1) * sizeof(uint32_t);
+}
+
+int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets,
+                        uint64_t* counters, void* workspace, void* stream) {
+    if (!counters || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS) return RPKT_E_INVAL;
+    if (n == 0) return RPKT_OK;
+    if (!ev) return RPKT_E_INVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (n_buckets > kFlowLdsMax) {
+        hipLaunchKernelGGL(flow_atomic_kernel, dim3(1024), dim3(256), 0, st, ev, n, n_buckets,
+                           (unsigned long long*)counters);
+        return hip_check(hipGetLastError());
+    }
+    if (!workspace) return RPKT_E_INVAL;
+    const uint32_t slabs = flow_blocks(n);
+    const uint32_t per = (n + slabs - 1) / slabs;
+    const size_t lds = 3 * (size_t)(n_buckets + 1) * sizeof(uint32_t);
+    static bool attr_set = false;
+    if (!attr_set) {
+        int rc0 = hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+        if (rc0) return rc0;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(flow_hist_kernel, dim3(slabs), dim3(kFlowThreads), lds, st, ev, n, per,
+                       n_buckets, (uint32_t*)workspace);
+    int rc = hip_check(hipGetLastError());
+    if (rc) return rc;
+    const uint32_t rows = n_buckets + 1;
+    hipLaunchKernelGGL(flow_reduce_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                       (const uint32_t*)workspace, slabs, n_buckets, counters);
+    return hip_check(hipGetLastError());
+}
+
+int rpkt_gpu_checksum_ranges(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* ranges,
+                             uint32_t n, uint16_t* out, void* stream) {
+    if (n == 0) return RPKT_OK;
+    if (!buf || !ranges || !out) return RPKT_E_INVAL;
+    if (buf_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    hipLaunchKernelGGL(checksum_ranges_kernel, dim3((n + per_block - 1) / per_block),
+                       dim3(per_block), 0, (hipStream_t)stream, buf, (uint32_t)buf_bytes, ranges,
+                       n, out);
+    return hip_check(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+"""Device batch API: rpkt's decode-and-verify chain over a device-resident batch.
+
+Thin ctypes layer over the C ABI in include/rpkt_gpu.h (librpkt_gpu.so, HIP for
+gfx950).  torch supplies device memory and the current HIP stream only; no torch
+type crosses the ABI.  There is no CPU fallback: if the HIP library is missing
+or no GPU is visible, every call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .build import GPU_LIB
+from .records import REC_BYTES, F_FLOW_EV
+
+RPKT_OK = 0
+ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN"}
+
+
+class RpktError(RuntimeError):
+    pass
+
+
+class Batch(ctypes.Structure):
+    """rpkt_batch_t"""
+    _fields_ = [("frames_dev", ctypes.c_void_p), ("frames_bytes", ctypes.c_uint64),
+                ("offsets_dev", ctypes.c_void_p), ("stride", ctypes.c_uint32),
+                ("frame_len", ctypes.c_uint32), ("n", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
+           "rpkt_gpu_last_hip_error", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
+           "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash"]
+
+_lib = None
+
+
+def lib():
+    """Load librpkt_gpu.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(GPU_LIB):
+            raise RpktError("HIP engine not built: %s missing (run __graft_entry__.build())"
+                            % GPU_LIB)
+        L = ctypes.CDLL(GPU_LIB)
+        L.rpkt_gpu_abi_version.restype = ctypes.c_uint32
+        L.rpkt_gpu_build_info.restype = ctypes.c_char_p
+        L.rpkt_gpu_status_name.argtypes = [ctypes.c_int]
+        L.rpkt_gpu_status_name.restype = ctypes.c_char_p
+        L.rpkt_gpu_last_hip_error.restype = ctypes.c_int
+        L.rpkt_gpu_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p]
+        L.rpkt_gpu_parse_batch.restype = ctypes.c_int
+        L.rpkt_gpu_flow_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.rpkt_gpu_flow_workspace_bytes.restype = ctypes.c_size_t
+        L.rpkt_gpu_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_flow_count.restype = ctypes.c_int
+        L.rpkt_gpu_checksum_ranges.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_checksum_ranges.restype = ctypes.c_int
+        L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
+                                     ctypes.c_uint16, ctypes.c_uint8]
+        L.rpkt_flow_hash.restype = ctypes.c_uint32
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != RPKT_OK:
+        extra = ""
+        if rc == -2:
+            extra = " (hipError %d)" % lib().rpkt_gpu_last_hip_error()
+        raise RpktError("%s failed: %s%s" % (what, ERRORS.get(rc, rc), extra))
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RpktError("no GPU visible: the rpkt_amd engine has no CPU path")
+    return torch
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class DeviceBatch:
+    """A batch resident in HBM: frames (uint8) and, for packed layout, u32 offsets."""
+
+    def __init__(self, frames, n, offsets=None, stride=0, frame_len=0):
+        self.frames, self.n, self.offsets = frames, n, offsets
+        self.stride, self.frame_len = stride, frame_len
+
+    @classmethod
+    def from_host(cls, hb, device="cuda"):
+        torch = _torch()
+        frames = torch.from_numpy(np.ascontiguousarray(hb.frames)).to(device)
+        offs = None
+        if hb.offsets is not None:
+            offs = torch.from_numpy(hb.offsets.view(np.int32)).to(device)
+        return cls(frames, hb.n, offs, hb.stride, hb.frame_len)
+
+    def shard(self, lo, hi):
+        """Frames [lo, hi) as a view (packed offsets stay absolute: no copy)."""
+        if self.offsets is not None:
+            return DeviceBatch(self.frames, hi - lo, self.offsets[lo:hi + 1])
+        return DeviceBatch(self.frames[lo * self.stride:], hi - lo, None, self.stride,
+                           self.frame_len)
+
+    def desc(self):
+        return Batch(self.frames.data_ptr(), self.frames.numel(),
+                     self.offsets.data_ptr() if self.offsets is not None else None,
+                     self.stride, self.frame_len, self.n, 0)
+
+
+def alloc_records(n, device="cuda"):
+    torch = _torch()
+    return torch.empty(n * REC_BYTES, dtype=torch.uint8, device=device)
+
+
+def parse_batch(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):
+    """rpkt_gpu_parse_batch: returns the uint8 record tensor (n * 80 bytes)."""
+    torch = _torch()
+    if recs is None:
+        recs = alloc_records(batch.n, batch.frames.device)
+    if flags & F_FLOW_EV and flow_ev is None:
+        flow_ev = torch.empty(batch.n, dtype=torch.int64, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_parse_batch(ctypes.byref(d), flags, recs.data_ptr(),
+                                    flow_ev.data_ptr() if flow_ev is not None else None,
+                                    n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_batch")
+    return (recs, flow_ev) if flags & F_FLOW_EV else recs
+
+
+def flow_workspace(n, n_buckets, device="cuda"):
+    torch = _torch()
+    nb = int(lib().rpkt_gpu_flow_workspace_bytes(n, n_buckets))
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
+
+
+def flow_count(flow_ev, n, n_buckets, counters=None, workspace=None, stream=None):
+    """rpkt_gpu_flow_count: counters u64[(n_buckets+1)*4] (+= into `counters`)."""
+    torch = _torch()
+    dev = flow_ev.device
+    if counters is None:
+        counters = torch.zeros((n_buckets + 1) * 4, dtype=torch.int64, device=dev)
+    if workspace is None:
+        workspace = flow_workspace(n, n_buckets, dev)
+    rc = lib().rpkt_gpu_flow_count(flow_ev.data_ptr(), n, n_buckets, counters.data_ptr(),
+                                   workspace.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_flow_count")
+    return counters
+
+
+def checksum_ranges(buf, ranges, out=None, stream=None):
+    """rpkt_gpu_checksum_ranges: batched checksum::from_slice over (start, len) pairs."""
+    torch = _torch()
+    n = ranges.numel() // 2
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=buf.device)
+    rc = lib().rpkt_gpu_checksum_ranges(buf.data_ptr(), buf.numel(), ranges.data_ptr(), n,
+                                        out.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_checksum_ranges")
+    return out

@@ -1,0 +1,91 @@
+"""The C-ABI library builds, loads and exports exactly what include/rpkt_gpu.h
+declares.  CPU only: no call here reaches a kernel launch."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from rpkt_amd import engine, records
+from rpkt_amd.build import build_gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "rpkt_gpu.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rpkt_\w+)\s*\(", src)) - {"rpkt_rec", "rpkt_batch"})
+
+
+@pytest.fixture(scope="module")
+def L():
+    build_gpu()
+    return engine.lib()
+
+
+def test_every_declared_symbol_is_exported(L):
+    names = declared_functions()
+    assert len(names) >= 9
+    for name in names:
+        assert hasattr(L, name), name
+    assert sorted(engine.EXPORTS) == names
+
+
+def test_abi_version_and_info(L):
+    assert L.rpkt_gpu_abi_version() == 1
+    assert b"gfx950" in L.rpkt_gpu_build_info()
+
+
+def test_status_names_match_records(L):
+    for name, code in records.STATUS.items():
+        assert L.rpkt_gpu_status_name(code).decode() == name
+    assert L.rpkt_gpu_status_name(99) == b"?"
+
+
+def test_record_layout_matches_header():
+    src = open(HDR).read()
+    fields = re.findall(r"/\*\s*(\d+)\s*(?:enum|[a-z]|\s)", src)
+    offs = [int(m) for m in re.findall(r";\s*/\*\s*(\d+) ", src)]
+    assert offs == [records.REC_DTYPE.fields[n][1] for n in records.REC_DTYPE.names]
+    assert records.REC_BYTES == 80 and fields
+
+
+def test_flow_hash_matches_oracle(L):
+    from oracle import oracle
+    import numpy as np
+    rng = np.random.default_rng(3)
+    for _ in range(500):
+        a, b = (int(x) for x in rng.integers(0, 2**32, 2))
+        sp, dp = (int(x) for x in rng.integers(0, 2**16, 2))
+        pr = int(rng.integers(0, 256))
+        assert L.rpkt_flow_hash(a, b, sp, dp, pr) == oracle.flow_hash(a, b, sp, dp, pr)
+
+
+def test_argument_validation_without_launch(L):
+    d = engine.Batch(None, 0, None, 64, 0, 0, 0)
+    assert L.rpkt_gpu_parse_batch(None, 3, None, None, 0, None) == -1      # NULL batch
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 3, 16, None, 0, None) == 0   # n == 0
+    d.n = 10
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 3, 16, None, 0, None) == -1  # NULL frames
+    d.frames_dev = 4096
+    d.frames_bytes = 1 << 32
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 3, 16, None, 0, None) == -3  # > 4 GiB
+    d.frames_bytes = 640
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 3, 8, None, 0, None) == -4   # misaligned
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 0x80, 16, None, 0, None) == -1  # bad flag
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 7, 16, None, 0, None) == -1  # FLOW_EV, NULL
+    d.stride = 0
+    assert L.rpkt_gpu_parse_batch(ctypes.byref(d), 3, 16, None, 0, None) == -1  # no layout
+    assert L.rpkt_gpu_flow_count(None, 10, 0, None, None, None) == -1
+    assert L.rpkt_gpu_checksum_ranges(None, 0, None, 0, None, None) == 0
+    assert L.rpkt_gpu_flow_workspace_bytes(1 << 20, 8192) > 0
+
+
+def test_engine_refuses_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(engine.RpktError):
+        engine.alloc_records(4)

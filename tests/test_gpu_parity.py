@@ -1,0 +1,209 @@
+"""GPU parity: every record byte of the HIP path equals the oracle's on the same
+buffers (bit-exact; integer/byte work has no tolerance), at the BASELINE.json
+full sizes and on the edge cases rpkt's own tests exercise."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from rpkt_amd import engine, gen
+from rpkt_amd.records import REC_DTYPE, STATUS, F_FLOW_EV, as_records
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKTS = os.path.join(HERE, "golden", "packets")
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need an MI355X"
+    return t
+
+
+def gpu_records(hb, flags=3, n_buckets=0):
+    db = engine.DeviceBatch.from_host(hb)
+    if flags & F_FLOW_EV:
+        recs, ev = engine.parse_batch(db, flags, n_buckets=n_buckets)
+        return as_records(recs.cpu().numpy()), ev.cpu().numpy().view(np.uint64)
+    return as_records(engine.parse_batch(db, flags).cpu().numpy())
+
+
+def oracle_records(hb, flags=3, n_buckets=0, flow=False):
+    return oracle.parse_batch(hb.frames, hb.n, flags=flags, offsets=hb.offsets,
+                              stride=hb.stride, frame_len=hb.frame_len, n_buckets=n_buckets,
+                              threads=THREADS, flow_ev=flow)
+
+
+def assert_same(g, o):
+    if g.tobytes() == o.tobytes():
+        return
+    bad = np.nonzero(g.view(np.uint8).reshape(-1, 80) != o.view(np.uint8).reshape(-1, 80))
+    i = int(bad[0][0])
+    fields = [f for f in REC_DTYPE.names if not np.array_equal(g[i][f], o[i][f])]
+    raise AssertionError("%d records differ; first #%d fields %s gpu=%s oracle=%s" % (
+        len(np.unique(bad[0])), i, fields, [g[i][f] for f in fields], [o[i][f] for f in fields]))
+
+
+def host_batch(frames_list, lead=0):
+    """Packed HostBatch from a list of byte strings; a `lead`-byte junk frame first
+    shifts every following frame's alignment."""
+    parts = ([b"\xee" * lead] if lead else []) + list(frames_list)
+    lens = np.array([len(p) for p in parts], dtype=np.uint64)
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    return gen.HostBatch(0, len(parts), 0, blob, offs.astype(np.uint32), 0, 0)
+
+
+# ---- full-size BASELINE configs --------------------------------------------------
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+def test_parity_baseline_configs(torch, cfg):
+    hb = gen.make_batch(cfg)
+    flags = 3
+    g = gpu_records(hb, flags)
+    o = oracle_records(hb, flags)
+    assert_same(g, o)
+    if cfg in (2, 3, 4):
+        assert (g["status"] == STATUS["OK"]).all()
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [3, 5, 6])
+def test_parity_flag_combinations(torch, cfg, flags):
+    hb = gen.make_batch(cfg, 50000, seed=100 + cfg)
+    assert_same(gpu_records(hb, flags), oracle_records(hb, flags))
+
+
+def test_parity_flow_events_and_counters(torch):
+    hb = gen.make_batch(4, 1 << 20, seed=41)
+    nb = 8192
+    g, gev = gpu_records(hb, 3 | F_FLOW_EV, nb)
+    o, oev = oracle_records(hb, 3, nb, flow=True)
+    assert_same(g, o)
+    assert np.array_equal(gev, oev)
+    dev = torch.from_numpy(gev.view(np.int64)).cuda()
+    c = engine.flow_count(dev, hb.n, nb).cpu().numpy().view(np.uint64)
+    assert np.array_equal(c, oracle.flow_count(oev, nb))
+    # calls accumulate
+    c2 = engine.flow_count(dev, hb.n, nb, counters=torch.from_numpy(c.view(np.int64)).cuda())
+    assert np.array_equal(c2.cpu().numpy().view(np.uint64), 2 * oracle.flow_count(oev, nb))
+
+
+def test_flow_counters_large_bucket_count(torch):
+    hb = gen.make_batch(4, 200000, seed=43)
+    nb = 50000                                     # beyond the LDS-privatised range
+    g, gev = gpu_records(hb, 3 | F_FLOW_EV, nb)
+    _, oev = oracle_records(hb, 3, nb, flow=True)
+    assert np.array_equal(gev, oev)
+    dev = torch.from_numpy(gev.view(np.int64)).cuda()
+    c = engine.flow_count(dev, hb.n, nb).cpu().numpy().view(np.uint64)
+    assert np.array_equal(c, oracle.flow_count(oev, nb))
+
+
+# ---- reference fixtures at every alignment ---------------------------------------
+
+def fixtures():
+    names = sorted(f for f in os.listdir(PKTS) if f.endswith(".dat"))
+    return names, [oracle.load_dat(os.path.join(PKTS, f)) for f in names]
+
+
+@pytest.mark.parametrize("lead", list(range(16)))
+def test_fixtures_every_alignment(torch, lead):
+    names, frames = fixtures()
+    hb = host_batch(frames, lead)
+    g, o = gpu_records(hb), oracle_records(hb)
+    assert_same(g, o)
+    base = 1 if lead else 0
+    i = base + names.index("TcpPacketWithOptions2.dat")
+    assert g[i]["ip_sum"] == 0xffff and g[i]["l4_sum"] == 0xffff
+
+
+def test_views_over_gpu_records(torch):
+    from rpkt_amd.views import EtherFrame, Ipv4, Udp, Packet, EtherType, IpProtocol
+    frame = oracle.load_dat(os.path.join(PKTS, "bench_frame.dat"))
+    g = gpu_records(host_batch([frame] * 3))
+    eth = EtherFrame.parse(Packet(g[1], frame)).unwrap()
+    assert eth.ethertype() == EtherType.IPV4
+    ip = Ipv4.parse(eth.payload()).unwrap()
+    assert ip.protocol() == IpProtocol.UDP and ip.ident() == 0x5c65 and ip.checksum() == 0
+    udp = Udp.parse(ip.payload()).unwrap()
+    assert (udp.src_port(), udp.dst_port(), udp.packet_len(), udp.checksum()) == \
+        (60376, 161, 74, 0xbc86)
+    assert udp.payload().chunk() == frame[42:108]
+
+
+# ---- edge cases --------------------------------------------------------------------
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
+def test_ragged_batch_sizes(torch, n):
+    hb = gen.make_batch(6, n, seed=n)
+    assert_same(gpu_records(hb), oracle_records(hb))
+
+
+def test_empty_batch(torch):
+    db = engine.DeviceBatch(torch.zeros(16, dtype=torch.uint8, device="cuda"), 0, None, 64)
+    out = engine.alloc_records(1)
+    engine.parse_batch(db, 3, recs=out)          # no launch, no error
+
+
+def test_unpadded_buffer_end(torch):
+    """Last frame ends at the last byte of an allocation that is not a multiple of 16."""
+    for cfg in (3, 5, 6):
+        hb = gen.make_batch(cfg, 777, seed=9)
+        hb.frames = hb.frames[:int(hb.offsets[-1])] if hb.offsets is not None else hb.frames
+        assert_same(gpu_records(hb), oracle_records(hb))
+
+
+def test_descriptor_past_buffer_is_clamped(torch):
+    hb = gen.make_batch(6, 1000, seed=5)
+    offs = hb.offsets.copy()
+    offs[500] = offs[-1] + 1000                  # one frame starts past the end
+    offs[700] = offs[699] - 5                    # one negative length
+    hb.offsets = offs
+    assert_same(gpu_records(hb), oracle_records(hb))
+
+
+def test_jumbo_and_max_length_frames(torch):
+    rng = np.random.default_rng(1)
+    frames = []
+    for L in (9000, 9001, 16384, 65535, 65549):
+        base = gen.make_batch(3, 1, seed=L)          # 1500-B TCP frame as a template
+        f = bytearray(base.frames.tobytes()) + bytearray(rng.integers(0, 256, L - 1500,
+                                                                      dtype=np.uint8).tobytes())
+        tot = min(L - 14, 65535)
+        f[16:18] = bytes([tot >> 8, tot & 0xff])
+        frames.append(bytes(f))
+    hb = host_batch(frames, lead=3)
+    g, o = gpu_records(hb), oracle_records(hb)
+    assert_same(g, o)
+    assert (g["status"][1:] == 0).all()
+
+
+def test_repeat_launches_identical(torch):
+    hb = gen.make_batch(5, 100000, seed=77)
+    db = engine.DeviceBatch.from_host(hb)
+    a = engine.parse_batch(db, 3).cpu().numpy()
+    for _ in range(3):
+        assert np.array_equal(engine.parse_batch(db, 3).cpu().numpy(), a)
+
+
+def test_checksum_ranges_match_from_slice(torch):
+    rng = np.random.default_rng(2)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    n = 20000
+    starts = rng.integers(0, buf.size, n)
+    lens = rng.integers(0, 4000, n)
+    lens[::10] = rng.integers(0, 20, n // 10)
+    lens[::97] = 65535
+    lens = np.minimum(lens, buf.size - starts)
+    ranges = np.stack([starts, lens], 1).astype(np.uint32)
+    out = engine.checksum_ranges(torch.from_numpy(buf).cuda(),
+                                 torch.from_numpy(ranges.view(np.int32)).cuda())
+    got = out.cpu().numpy().view(np.uint16)
+    want = [oracle.from_slice(buf[s:s + l]) for s, l in ranges[:3000]]
+    assert got[:3000].tolist() == want
