@@ -171,6 +171,8 @@ const char* rpkt_gpu_build_info(void);
 const char* rpkt_gpu_status_name(int status);
 /* Last HIP error code seen by this thread (hipError_t as int), 0 if none. */
 int rpkt_gpu_last_hip_error(void);
+/* Human-readable runtime/device description into buf (diagnostics). */
+int rpkt_gpu_device_info(char* buf, size_t len);
 
 /* Parse + verify a batch.  Replaces, per frame i, the reference sequence
  *   EtherFrame::parse -> [VlanFrame::parse]* -> Ipv4::parse -> Udp|Tcp::parse

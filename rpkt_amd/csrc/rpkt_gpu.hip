@@ -26,6 +26,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
+
+#include <tuple>
 
 #include "../../include/rpkt_gpu.h"
 
@@ -62,8 +65,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
                                              0x00020000);
 }
 
-__device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+// 16 bytes at `off` of a buffer of `limit` bytes: bytes at or past `limit` read as 0.
+// A dwordx4 that straddles the range end is dropped whole by the hardware range
+// check, so the (at most one per buffer) straddling chunk is read byte by byte.
+__device__ __attribute__((noinline)) u32x4 load16_tail(__amdgpu_buffer_rsrc_t r, uint32_t off,
+                                                        uint32_t limit) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        uint32_t b = off + k < limit
+                         ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(off + k), 0, 0)
+                         : 0u;
+        v[k >> 2] |= b << (8 * (k & 3));
+    }
+    return v;
+}
+
+__device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t limit) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (off + 16u <= limit) v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    else if (off < limit) v = load16_tail(r, off, limit);
+    return v;
 }
 
 // Inclusive prefix sum over the 64 lanes (DPP: row shifts then row broadcasts).
@@ -126,7 +148,7 @@ __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* lds, uint32_t s
 // Flattened chunk stream over the tile: lane q owns absolute byte range
 // [s_abs, e_abs) (empty allowed); returns that range's absolute-phase word sum.
 // Consecutive lanes read consecutive 16-byte chunks of the concatenated ranges.
-// `oob` is the descriptor's byte range: a voffset there loads zeros, no traffic.
+// `oob` is the descriptor's byte range (loads at or past it return zeros).
 __device__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob, uint32_t s_abs,
                                     uint32_t e_abs, WaveScratch& W, int lane) {
     uint32_t nch = e_abs > s_abs ? ((e_abs - 1) >> 4) - (s_abs >> 4) + 1 : 0;
@@ -154,7 +176,7 @@ __device__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob, uin
                 if (W.pref[lo + step] <= c) lo += step;
             q[u] = lo;
             a[u] = ((W.s[lo] & ~15u) + 16u * (c - W.pref[lo]));
-            d[u] = load16(rs, c < total ? a[u] : oob);
+            d[u] = load16(rs, c < total ? a[u] : oob, oob);
         }
 #pragma unroll
         for (int u = 0; u < kStreamUnroll; ++u) {
@@ -241,7 +263,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
             const uint32_t q = c / kWinChunks, j = c % kWinChunks;
             const uint32_t qo = W.fo[q], ql = W.fl[q];
             const uint32_t a = (qo & ~15u) + 16u * j;
-            d[k] = load16(rs, (a < qo + ql) ? a : frames_bytes);
+            d[k] = load16(rs, (a < qo + ql) ? a : frames_bytes, frames_bytes);
         }
 #pragma unroll
         for (int k = 0; k < kWinChunks; ++k)
@@ -532,6 +554,21 @@ inline int hip_check(hipError_t e) {
     return RPKT_OK;
 }
 
+// Launch and report THIS launch's status (hipGetLastError would also return
+// errors other libraries in the process left behind).
+template <typename... KArgs, typename... Args>
+int launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t st,
+           Args... args) {
+    static_assert(sizeof...(KArgs) == sizeof...(Args), "kernel arity");
+    auto packed = std::tuple<KArgs...>(static_cast<KArgs>(args)...);
+    void* argv[sizeof...(KArgs)];
+    std::apply([&](auto&... a) {
+        int k = 0;
+        ((argv[k++] = (void*)&a), ...);
+    }, packed);
+    return hip_check(hipLaunchKernel((const void*)kernel, grid, block, argv, lds, st));
+}
+
 }  // namespace
 
 extern "C" {
@@ -551,6 +588,22 @@ const char* rpkt_gpu_status_name(int s) {
 }
 
 int rpkt_gpu_last_hip_error(void) { return g_last_hip_error; }
+
+int rpkt_gpu_device_info(char* buf, size_t len) {
+    int count = 0, dev = -1;
+    hipError_t e1 = hipGetDeviceCount(&count);
+    hipError_t e2 = hipGetDevice(&dev);
+    hipDeviceProp_t p;
+    memset(&p, 0, sizeof(p));
+    hipError_t e3 = dev >= 0 ? hipGetDeviceProperties(&p, dev) : hipErrorInvalidDevice;
+    int rv = 0;
+    if (hipRuntimeGetVersion(&rv) != hipSuccess) rv = -1;
+    if (buf && len)
+        snprintf(buf, len, "hip_runtime=%d devices=%d(err %d) current=%d(err %d) name=%s arch=%s "
+                 "cus=%d (err %d)", rv, count, (int)e1, dev, (int)e2, p.name, p.gcnArchName,
+                 p.multiProcessorCount, (int)e3);
+    return (e1 == hipSuccess && count > 0) ? RPKT_OK : RPKT_E_HIP;
+}
 
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_t dp,
                         uint8_t proto) {
@@ -584,10 +637,9 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    hipLaunchKernelGGL(parse_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
-                       b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen,
-                       b->n, flags, recs_dev, flow_ev_dev, n_buckets);
-    return hip_check(hipGetLastError());
+    return launch(parse_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen,
+                  b->n, flags, recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
 }
 
 size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets) {
@@ -602,9 +654,8 @@ int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets
     if (!ev) return RPKT_E_INVAL;
     hipStream_t st = (hipStream_t)stream;
     if (n_buckets > kFlowLdsMax) {
-        hipLaunchKernelGGL(flow_atomic_kernel, dim3(1024), dim3(256), 0, st, ev, n, n_buckets,
-                           (unsigned long long*)counters);
-        return hip_check(hipGetLastError());
+        return launch(flow_atomic_kernel, dim3(1024), dim3(256), 0, st, (const uint64_t*)ev, n,
+                      n_buckets, (unsigned long long*)counters);
     }
     if (!workspace) return RPKT_E_INVAL;
     const uint32_t slabs = flow_blocks(n);
@@ -618,14 +669,12 @@ int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets
         if (rc0) return rc0;
         attr_set = true;
     }
-    hipLaunchKernelGGL(flow_hist_kernel, dim3(slabs), dim3(kFlowThreads), lds, st, ev, n, per,
-                       n_buckets, (uint32_t*)workspace);
-    int rc = hip_check(hipGetLastError());
+    int rc = launch(flow_hist_kernel, dim3(slabs), dim3(kFlowThreads), lds, st,
+                    (const uint64_t*)ev, n, per, n_buckets, (uint32_t*)workspace);
     if (rc) return rc;
     const uint32_t rows = n_buckets + 1;
-    hipLaunchKernelGGL(flow_reduce_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
-                       (const uint32_t*)workspace, slabs, n_buckets, counters);
-    return hip_check(hipGetLastError());
+    return launch(flow_reduce_kernel, dim3((rows + 255) / 256), dim3(256), 0, st,
+                  (const uint32_t*)workspace, slabs, n_buckets, counters);
 }
 
 int rpkt_gpu_checksum_ranges(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* ranges,
@@ -634,10 +683,8 @@ int rpkt_gpu_checksum_ranges(const uint8_t* buf, uint64_t buf_bytes, const uint3
     if (!buf || !ranges || !out) return RPKT_E_INVAL;
     if (buf_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
     const uint32_t per_block = kWave * kWavesPerBlock;
-    hipLaunchKernelGGL(checksum_ranges_kernel, dim3((n + per_block - 1) / per_block),
-                       dim3(per_block), 0, (hipStream_t)stream, buf, (uint32_t)buf_bytes, ranges,
-                       n, out);
-    return hip_check(hipGetLastError());
+    return launch(checksum_ranges_kernel, dim3((n + per_block - 1) / per_block), dim3(per_block),
+                  0, (hipStream_t)stream, buf, (uint32_t)buf_bytes, ranges, n, out);
 }
 
 }  // extern "C"

@@ -30,7 +30,7 @@ class Batch(ctypes.Structure):
 
 
 EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
-           "rpkt_gpu_last_hip_error", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
+           "rpkt_gpu_last_hip_error", "rpkt_gpu_device_info", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash"]
 
 _lib = None
@@ -40,6 +40,10 @@ def lib():
     """Load librpkt_gpu.so (fails loudly: there is no fallback path)."""
     global _lib
     if _lib is None:
+        # Bind to the HIP runtime torch already carries: loading ours first would
+        # pull a second runtime (/opt/rocm) into the process, and only one of the
+        # two can own the device.
+        import torch  # noqa: F401
         if not os.path.exists(GPU_LIB):
             raise RpktError("HIP engine not built: %s missing (run __graft_entry__.build())"
                             % GPU_LIB)
@@ -49,6 +53,8 @@ def lib():
         L.rpkt_gpu_status_name.argtypes = [ctypes.c_int]
         L.rpkt_gpu_status_name.restype = ctypes.c_char_p
         L.rpkt_gpu_last_hip_error.restype = ctypes.c_int
+        L.rpkt_gpu_device_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.rpkt_gpu_device_info.restype = ctypes.c_int
         L.rpkt_gpu_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p]
@@ -66,6 +72,12 @@ def lib():
         L.rpkt_flow_hash.restype = ctypes.c_uint32
         _lib = L
     return _lib
+
+
+def device_info():
+    buf = ctypes.create_string_buffer(512)
+    lib().rpkt_gpu_device_info(buf, 512)
+    return buf.value.decode()
 
 
 def _check(rc, what):
