@@ -78,8 +78,8 @@ def algorithmic_bytes(hb):
 
 def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
     """Time `steps` launches (rotating over dbs).  Returns wall seconds (max over
-    ranks) and the mean per-launch kernel duration from HIP events recorded on the
-    launch stream around each launch."""
+    ranks) and the mean per-launch device time from two HIP events recorded on the
+    launch stream around the back-to-back launches."""
     stream = torch.cuda.current_stream()
     R = len(dbs)
     nb = flow["n_buckets"] if flow else 0
@@ -96,20 +96,20 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
 
     for k in range(warmup):
         one(k)
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(steps):
-        ev0[k].record(stream)
         one(k)
-        ev1[k].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev0, ev1)]))
+    kern_ms = ev0.elapsed_time(ev1) / steps      # back-to-back launches on `stream`
     return wall, kern_ms
 
 

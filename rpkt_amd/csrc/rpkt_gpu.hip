@@ -40,19 +40,20 @@ constexpr int kWave = 64;            // lanes per wavefront (CDNA)
 constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
 constexpr int kWin = 128;            // header window bytes per frame in LDS
 constexpr int kWinChunks = kWin / 16;
+constexpr int kSlot = kWin + 4;      // LDS slot stride: 33 dwords, so lane-strided
+                                     // reads of the 64 slots hit 32 distinct banks
 constexpr int kStreamUnroll = 4;     // 16-B chunk loads in flight per lane per step
 constexpr uint64_t kMaxFrameBytes = 0xffffff00ull;  // voffset + 16 never wraps
 
-struct WaveScratch {
-    uint8_t  win[kWave * kWin];      // 8 KiB header windows
-    uint32_t fo[kWave];              // frame offsets
-    uint32_t fl[kWave];              // frame lengths
+struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit a CU
+    uint8_t  win[kWave * kSlot];     // header windows, slot stride 132 B
+    uint32_t s[kWave];               // window phase: frame offset; stream: range start
+    uint32_t e[kWave];               // window phase: frame length; stream: range end
     uint32_t pref[kWave + 1];        // stream: exclusive prefix of chunk counts
-    uint32_t s[kWave];               // stream: range start (absolute byte)
-    uint32_t e[kWave];               // stream: range end (absolute byte)
     uint32_t first[kWave];           // stream: scan value before a range's first chunk
     uint32_t last[kWave];            // stream: scan value at a range's last chunk
 };
+static_assert(sizeof(WaveScratch) * kWavesPerBlock * 4 <= 160 * 1024, "4 blocks per CU");
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -67,9 +68,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 
 // 16 bytes at `off` of a buffer of `limit` bytes: bytes at or past `limit` read as 0.
 // A dwordx4 that straddles the range end is dropped whole by the hardware range
-// check, so the (at most one per buffer) straddling chunk is read byte by byte.
-__device__ __attribute__((noinline)) u32x4 load16_tail(__amdgpu_buffer_rsrc_t r, uint32_t off,
-                                                        uint32_t limit) {
+// check, so the (at most one per buffer) straddling chunk is read as the last 16
+// in-range bytes and shifted down.
+__device__ __forceinline__ u32x4 load16_bytes(__amdgpu_buffer_rsrc_t r, uint32_t off,
+                                                         uint32_t limit) {
     u32x4 v = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
@@ -81,10 +83,32 @@ __device__ __attribute__((noinline)) u32x4 load16_tail(__amdgpu_buffer_rsrc_t r,
     return v;
 }
 
+// Branch-free main-path load: out-of-range and straddling chunks read as zeros (the
+// caller patches a straddling chunk with load16_fix on a rare, separate path, so the
+// hot loops carry no data-dependent vmcnt waits).
+__device__ __forceinline__ u32x4 load16_fast(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+}
+
+__device__ __forceinline__ bool straddles(uint32_t off, uint32_t limit) {
+    return off < limit && off + 16u > limit;
+}
+
 __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t limit) {
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (off + 16u <= limit) v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
-    else if (off < limit) v = load16_tail(r, off, limit);
+    if (off + 16u <= limit) {
+        v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    } else if (off < limit) {
+        if (__builtin_expect(limit >= 16u, 1)) {
+            u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(limit - 16u), 0, 0);
+            unsigned __int128 x = (unsigned __int128)t.x | ((unsigned __int128)t.y << 32) |
+                                  ((unsigned __int128)t.z << 64) | ((unsigned __int128)t.w << 96);
+            x >>= 8u * (16u - (limit - off));
+            v = u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+        } else {
+            v = load16_bytes(r, off, limit);
+        }
+    }
     return v;
 }
 
@@ -134,26 +158,76 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
            halves(d.z & byte_mask(lo - 8, hi - 8)) + halves(d.w & byte_mask(lo - 12, hi - 12));
 }
 
-// Word sum of LDS bytes [s, e) (LDS byte addresses with the frame's absolute phase).
-__device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* lds, uint32_t s, uint32_t e) {
-    uint32_t acc = 0;
-    for (uint32_t a = s & ~3u; a < e; a += 4) {
-        uint32_t w = *reinterpret_cast<const uint32_t*>(lds + a);
-        w &= byte_mask((int)s - (int)a, (int)e - (int)a);
-        acc += halves(w);
-    }
-    return acc;
-}
-
 // Flattened chunk stream over the tile: lane q owns absolute byte range
 // [s_abs, e_abs) (empty allowed); returns that range's absolute-phase word sum.
-// Consecutive lanes read consecutive 16-byte chunks of the concatenated ranges.
-// `oob` is the descriptor's byte range (loads at or past it return zeros).
-__device__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob, uint32_t s_abs,
-                                    uint32_t e_abs, WaveScratch& W, int lane) {
-    uint32_t nch = e_abs > s_abs ? ((e_abs - 1) >> 4) - (s_abs >> 4) + 1 : 0;
-    uint32_t incl = wave_incl_scan(nch);
-    uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+// Consecutive lanes read consecutive 16-byte chunks of the concatenated ranges
+// (coalesced whatever the frame sizes).  Each chunk's word sum enters a wave-wide
+// inclusive scan; a range's sum is the scan value at its last chunk minus the value
+// before its first.  Loads are double-buffered: batch k+1 is in flight while batch k
+// is summed, and every batch issues unconditionally (lanes past the end read the
+// descriptor's out-of-range offset: zeros, no traffic) so the vmcnt waits stay exact.
+// `oob` is the descriptor's byte range.
+struct StreamBatch {
+    u32x4 d[kStreamUnroll];
+    uint32_t a[kStreamUnroll];       // chunk address
+    uint32_t q[kStreamUnroll];       // owning lane (range)
+};
+
+__device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
+                                             const WaveScratch& W, uint32_t total, uint32_t base,
+                                             int lane, uint32_t& cur, StreamBatch& B) {
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; ++u) {
+        const uint32_t c = base + u * kWave + lane;
+        // advance the lane's cursor to the range holding chunk c: ranges are in chunk
+        // order, so the cursor only moves forward; jump by binary search when far
+        if (W.pref[cur + 1] <= c) {
+            if (W.pref[cur + 2] > c) {
+                cur += 1;
+            } else {
+                uint32_t lo = 0;
+#pragma unroll
+                for (int step = 32; step; step >>= 1)
+                    if (W.pref[lo + step] <= c) lo += step;
+                cur = lo;
+            }
+        }
+        B.q[u] = cur;
+        B.a[u] = (W.s[cur] & ~15u) + 16u * (c - W.pref[cur]);
+        B.d[u] = load16_fast(rs, c < total ? B.a[u] : oob);
+    }
+}
+
+__device__ __forceinline__ void stream_consume(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
+                                               WaveScratch& W, uint32_t total, uint32_t base,
+                                               int lane, uint32_t& run, const StreamBatch& B) {
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; ++u) {
+        const uint32_t c = base + u * kWave + lane;
+        uint32_t v = 0;
+        const uint32_t q = B.q[u];
+        if (c < total) {
+            const int lo = (int)W.s[q] - (int)B.a[u];
+            const int hi = (int)W.e[q] - (int)B.a[u];
+            v = chunk_sum(B.d[u], lo, hi);
+            if (__builtin_expect(straddles(B.a[u], oob), 0))    // buffer's last chunk
+                v = chunk_sum(load16(rs, B.a[u], oob), lo, hi);
+        }
+        const uint32_t sc = wave_incl_scan(v) + run;
+        run = __builtin_amdgcn_readlane(sc, 63);
+        if (c < total) {
+            if (c == W.pref[q]) W.first[q] = sc - v;
+            if (c + 1 == W.pref[q + 1]) W.last[q] = sc;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
+                                                    uint32_t s_abs, uint32_t e_abs,
+                                                    WaveScratch& W, int lane) {
+    const uint32_t nch = e_abs > s_abs ? ((e_abs - 1) >> 4) - (s_abs >> 4) + 1 : 0;
+    const uint32_t incl = wave_incl_scan(nch);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
     if (total == 0) return 0;                                    // wave-uniform
     W.pref[lane] = incl - nch;
     if (lane == 63) W.pref[64] = incl;
@@ -163,37 +237,19 @@ __device__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob, uin
     W.last[lane] = 0;
     wave_sync();
 
-    uint32_t run = 0;                                            // scan carry (uniform)
-    for (uint32_t base = 0; base < total; base += kWave * kStreamUnroll) {
-        u32x4 d[kStreamUnroll];
-        uint32_t q[kStreamUnroll], a[kStreamUnroll];
-#pragma unroll
-        for (int u = 0; u < kStreamUnroll; ++u) {
-            uint32_t c = base + u * kWave + lane;
-            uint32_t lo = 0;
-#pragma unroll
-            for (int step = 32; step; step >>= 1)
-                if (W.pref[lo + step] <= c) lo += step;
-            q[u] = lo;
-            a[u] = ((W.s[lo] & ~15u) + 16u * (c - W.pref[lo]));
-            d[u] = load16(rs, c < total ? a[u] : oob, oob);
-        }
-#pragma unroll
-        for (int u = 0; u < kStreamUnroll; ++u) {
-            uint32_t c = base + u * kWave + lane;
-            uint32_t v = 0;
-            if (c < total) {
-                int lo = (int)W.s[q[u]] - (int)a[u];
-                int hi = (int)W.e[q[u]] - (int)a[u];
-                v = chunk_sum(d[u], lo, hi);
-            }
-            uint32_t sc = wave_incl_scan(v) + run;
-            run = __builtin_amdgcn_readlane(sc, 63);
-            if (c < total) {
-                if (c == W.pref[q[u]]) W.first[q[u]] = sc - v;
-                if (c + 1 == W.pref[q[u] + 1]) W.last[q[u]] = sc;
-            }
-        }
+    constexpr uint32_t kBatch = kWave * kStreamUnroll;
+    uint32_t run = 0, cur = 0;
+    StreamBatch A, B;
+    uint32_t base = 0;
+    stream_issue(rs, oob, W, total, base, lane, cur, A);
+    for (;;) {
+        stream_issue(rs, oob, W, total, base + kBatch, lane, cur, B);
+        stream_consume(rs, oob, W, total, base, lane, run, A);
+        if (base + kBatch >= total) break;
+        stream_issue(rs, oob, W, total, base + 2 * kBatch, lane, cur, A);
+        stream_consume(rs, oob, W, total, base + kBatch, lane, run, B);
+        if (base + 2 * kBatch >= total) break;
+        base += 2 * kBatch;
     }
     wave_sync();
     return nch ? W.last[lane] - W.first[lane] : 0;
@@ -233,6 +289,310 @@ __device__ __forceinline__ uint32_t flow_hash(uint32_t src, uint32_t dst, uint32
     return h;
 }
 
+// ---- per-frame parse state (registers) ----
+struct LaneRec {
+    uint32_t w[20];                  // the 80-byte rpkt_rec_t as 20 little-endian words
+    uint32_t status;
+    uint32_t stream_s, stream_e;     // absolute L4 bytes past the LDS window
+    uint32_t l4_part;                // in-window part of the L4 word sum
+    uint32_t l4_start_abs, pseudo;
+    bool want_l4;
+};
+
+// Window loads of one tile into registers: chunk c = k*64 + lane is piece c%8 of
+// frame c/8; a frame's offset/length come from its owning lane by ds_bpermute.
+// Returns a bit per k whose chunk straddles the end of the frames buffer.
+__device__ __forceinline__ uint32_t window_issue(__amdgpu_buffer_rsrc_t rs, uint32_t fb, Frame fr,
+                                                 int lane, u32x4 (&d)[kWinChunks],
+                                                 uint32_t (&addr)[kWinChunks]) {
+    uint32_t fix = 0;
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) {
+        const int c = k * kWave + lane;
+        const int q = c / kWinChunks, j = c % kWinChunks;
+        const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+        const uint32_t ql = (uint32_t)__shfl((int)fr.len, q, kWave);
+        const uint32_t a = (qo & ~15u) + 16u * j;
+        addr[k] = (a < qo + ql) ? a : fb;
+        fix |= (uint32_t)straddles(addr[k], fb) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+    return fix;
+}
+
+__device__ __forceinline__ void put_chunk(WaveScratch& W, int c, u32x4 v) {
+    uint32_t* dst =
+        reinterpret_cast<uint32_t*>(&W.win[(c / kWinChunks) * kSlot + (c % kWinChunks) * 16]);
+    dst[0] = v.x;
+    dst[1] = v.y;
+    dst[2] = v.z;
+    dst[3] = v.w;
+}
+
+// Registers -> LDS window slots (slot stride 132 B, so 4-byte stores).  A chunk that
+// straddles the buffer end (at most one per buffer) is then re-read exactly and
+// overwritten in LDS: the registers themselves are never modified conditionally.
+__device__ __forceinline__ void window_commit(WaveScratch& W, __amdgpu_buffer_rsrc_t rs,
+                                              uint32_t fb, const u32x4 (&d)[kWinChunks],
+                                              const uint32_t (&addr)[kWinChunks], uint32_t fix,
+                                              int lane) {
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) put_chunk(W, k * kWave + lane, d[k]);
+    if (__builtin_expect(__ballot(fix != 0) != 0, 0)) {
+        for (int k = 0; k < kWinChunks; ++k)
+            if (fix & (1u << k)) put_chunk(W, k * kWave + lane, load16(rs, addr[k], fb));
+    }
+}
+
+// ---- dword-granular LDS access for the parse ----
+// Frame byte x of this lane lives at LDS offset ph + x of its slot (ph = frame
+// offset & 15, the absolute 16-byte phase), so aligned LDS dwords are aligned in
+// absolute address too: the raw dwords feed the checksum sums directly, and
+// v_alignbyte turns them into frame-relative little-endian dwords for the getters.
+__device__ __forceinline__ uint32_t lds32(const uint8_t* slot, uint32_t a) {
+    return *reinterpret_cast<const uint32_t*>(slot + a);
+}
+__device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+// big-endian u16 from little-endian bytes 0,1 / 2,3 of a dword
+__device__ __forceinline__ uint32_t be16_lo(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c0c0001u); }
+__device__ __forceinline__ uint32_t be16_hi(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c0c0203u); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x00010203u); }
+
+// Read the 6 aligned LDS dwords covering frame bytes [x, x + 20) (any phase): raw
+// dwords R (absolute-aligned, for sums) and frame-relative dwords F (for getters).
+struct Hdr6 {
+    uint32_t a0;            // LDS offset of R[0]
+    uint32_t R[6];
+    uint32_t F[5];
+};
+__device__ __forceinline__ void read_hdr(const uint8_t* slot, uint32_t ldsx, Hdr6& h) {
+    h.a0 = ldsx & ~3u;
+    const uint32_t sh = ldsx & 3u;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) h.R[k] = lds32(slot, h.a0 + 4 * k);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h.F[k] = align_bytes(h.R[k + 1], h.R[k], sh);
+}
+
+// Word sum of LDS bytes [s, e) using the already-read raw dwords R[0..N) at a0,
+// continuing with LDS reads past them (IPv4 options, long in-window L4 spans).
+template <int N>
+__device__ __forceinline__ uint32_t raw_range_sum(const uint8_t* slot, const uint32_t (&R)[N],
+                                                  uint32_t a0, uint32_t s, uint32_t e) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int a = (int)(a0 + 4 * k);
+        acc += halves(R[k] & byte_mask((int)s - a, (int)e - a));
+    }
+    for (uint32_t a = a0 + 4 * N; a < e; a += 4)
+        acc += halves(lds32(slot, a) & byte_mask((int)s - (int)a, (int)e - (int)a));
+    return acc;
+}
+
+__device__ __forceinline__ bool is_tag(uint32_t et) { return et == 0x8100u || et == 0x88a8u; }
+
+// Lane-per-frame parse from the LDS window: the rpkt chain with every getter, the
+// IPv4 header sum and the in-window part of the L4 sum.  Three dependent rounds of
+// LDS dword reads: link layer (bytes 0..23), IPv4 header at l3, L4 header at l4.
+__device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame fr, bool valid,
+                                           uint32_t flags, LaneRec& L) {
+    const uint32_t ph = fr.off & 15u;
+    const uint8_t* slot = &W.win[lane * kSlot];
+    uint32_t* w = L.w;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    const uint32_t len = valid ? fr.len : 0u;
+    L.stream_s = L.stream_e = L.l4_part = L.l4_start_abs = L.pseudo = 0;
+    L.want_l4 = false;
+    w[19] = len;
+    uint32_t status = RPKT_S_OK;
+
+    // round 1: Ethernet + up to two 802.1Q/802.1ad tags, frame bytes [0, 24)
+    uint32_t E[6];
+    {
+        const uint32_t a0 = ph & ~3u, sh = ph & 3u;
+        uint32_t R[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) R[k] = lds32(slot, a0 + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) E[k] = align_bytes(R[k + 1], R[k], sh);
+    }
+    if (len < 14) {                                            // ether/generated.rs:36
+        L.status = RPKT_S_ETH_SHORT;
+        w[0] = RPKT_S_ETH_SHORT;
+        return;
+    }
+    w[1] = E[0];                                               // dst_addr, src_addr
+    w[2] = E[1];                                               //   ether/generated.rs:47-54
+    w[3] = E[2];
+    const uint32_t eth_et = be16_lo(E[3]);                     // ethertype :55-59
+    // VLAN walk (vlan/generated.rs:32-61), at most RPKT_MAX_VLAN tags
+    uint32_t nvlan = 0, et = eth_et;
+    if (is_tag(et)) {
+        if (len - 14 < 4) {
+            status = RPKT_S_VLAN_SHORT;
+        } else {
+            et = be16_lo(E[4]);
+            w[4] = be16_hi(E[3]);
+            w[5] = et;
+            nvlan = 1;
+            if (is_tag(et)) {
+                if (len - 18 < 4) {
+                    status = RPKT_S_VLAN_SHORT;
+                } else {
+                    et = be16_lo(E[5]);
+                    w[4] |= be16_hi(E[4]) << 16;
+                    w[5] |= et << 16;
+                    nvlan = 2;
+                }
+            }
+        }
+    }
+    w[0] = (nvlan << 8) | (eth_et << 16);
+    if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+
+    // round 2: Ipv4::parse (ipv4/generated.rs:35-51) and getters (:61-112, 269-288)
+    const uint32_t l3 = 14u + 4u * nvlan, rem = len - l3;
+    w[16] = l3;
+    Hdr6 ip;
+    read_hdr(slot, ph + l3, ip);
+    const uint32_t vhl = ip.F[0] & 0xffu;
+    const uint32_t ihl4 = (vhl & 0xfu) * 4u;
+    const uint32_t tot = be16_hi(ip.F[0]);
+    if (rem < 20) status = RPKT_S_IP_SHORT;
+    else if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
+    else if (ihl4 > rem) status = RPKT_S_IP_IHL_GT_LEN;
+    else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
+    else if (tot > rem) status = RPKT_S_IP_TOT_GT_LEN;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+    const uint32_t proto = (ip.F[2] >> 8) & 0xffu;
+    const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
+    w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
+    w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
+    w[8] = (ip.F[2] & 0xffffu) | (be16_hi(ip.F[2]) << 16);
+    w[9] = src;
+    w[10] = dst;
+    if (flags & RPKT_F_IP_SUM)
+        w[18] = be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4), fr.off + l3);
+    const uint32_t l4 = l3 + ihl4;                             // Ipv4::payload :115-127
+    const uint32_t l4rem = tot - ihl4;
+    w[16] |= l4 << 16;
+    w[17] = l4 | (l4rem << 16);
+
+    // round 3: Udp::parse (udp/generated.rs:31-42) / Tcp::parse (tcp/generated.rs:34-45)
+    Hdr6 h4;
+    read_hdr(slot, ph + l4, h4);
+    uint32_t l4len = 0;
+    if (proto == 17u) {
+        const uint32_t ulen = be16_lo(h4.F[1]);
+        if (l4rem < 8) status = RPKT_S_UDP_SHORT;
+        else if (ulen < 8 || ulen > l4rem) status = RPKT_S_UDP_BAD_LEN;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[14] = ulen;
+            w[15] = be16_hi(h4.F[1]);
+            w[17] = (l4 + 8) | ((ulen - 8) << 16);             // Udp::payload :66-76
+            l4len = ulen;
+        }
+    } else if (proto == 6u) {
+        const uint32_t hl = ((h4.F[3] >> 4) & 0xfu) * 4u;
+        if (l4rem < 20) status = RPKT_S_TCP_SHORT;
+        else if (hl < 20 || hl > l4rem) status = RPKT_S_TCP_BAD_DOFF;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[12] = bswap32(h4.F[1]);
+            w[13] = bswap32(h4.F[2]);
+            w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
+            w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
+            w[17] = (l4 + hl) | ((l4rem - hl) << 16);          // Tcp::payload :125-131
+            l4len = l4rem;
+        }
+    } else {
+        status = RPKT_S_L4_OTHER;
+    }
+    w[0] |= status;
+    L.status = status;
+    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+        L.want_l4 = true;
+        // pseudo header (smoltcp pseudo_header_v4): src, dst, proto, length
+        L.pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto + l4len;
+        const uint32_t win_end = kWin - ph;                    // frame offset where LDS ends
+        const uint32_t e = l4 + l4len;
+        const uint32_t e_in = e < win_end ? e : win_end;
+        L.l4_part = raw_range_sum(slot, h4.R, h4.a0, ph + l4, ph + e_in);
+        L.l4_start_abs = fr.off + l4;
+        if (e > win_end) {
+            L.stream_s = fr.off + win_end;
+            L.stream_e = fr.off + e;
+        }
+    }
+}
+
+// Flow event of a parsed frame (include/rpkt_gpu.h, rpkt_flow_ev_t).
+__device__ __forceinline__ uint64_t flow_event(const LaneRec& L, uint32_t n_buckets) {
+    const uint32_t* w = L.w;
+    uint64_t ev = w[19];
+    uint32_t bucket = n_buckets;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;
+    const bool ip_parsed = L.status == RPKT_S_OK || L.status >= RPKT_S_L4_OTHER;
+    if (L.status == RPKT_S_OK)
+        bucket = flow_hash(w[9], w[10], w[11] & 0xffffu, w[11] >> 16, proto) % n_buckets;
+    ev |= (uint64_t)bucket << 32;
+    if (ip_parsed && (w[18] & 0xffffu) != 0xffffu) ev |= 1ull << 48;
+    if (L.status == RPKT_S_OK && (w[18] >> 16) != 0xffffu &&
+        !(proto == 17u && (w[15] & 0xffffu) == 0))
+        ev |= 1ull << 49;
+    return ev;
+}
+
+// Records of the tile staged through LDS (stride 21 dwords: conflict-free writes) and
+// stored as 5 wave-instructions of 1 KiB contiguous each.
+__device__ __forceinline__ void store_records(WaveScratch& W, int lane, const uint32_t (&w)[20],
+                                              rpkt_rec_t* recs, uint32_t p0, uint32_t n) {
+    wave_sync();
+    uint32_t* rl = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+    for (int k = 0; k < 20; ++k) rl[lane * 21 + k] = w[k];
+    wave_sync();
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(recs + p0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+        const uint32_t* src = rl + r * 21 + pc * 4;
+        if (r < nrec) out[c] = u32x4{src[0], src[1], src[2], src[3]};
+    }
+}
+
+struct SpanSrc {
+    const uint32_t* offsets;
+    uint32_t stride, frame_len, fb, n;
+    __device__ __forceinline__ Frame get(uint32_t i) const {
+        if (i >= n) return Frame{0, 0};
+        return frame_span(offsets, stride, frame_len, fb, i);
+    }
+};
+
+// One wavefront per 64-frame tile: window loads -> LDS, lane-per-frame parse,
+// flattened L4 stream, LDS-staged coalesced record stores.  (A persistent variant
+// that prefetched the next tile's window into registers measured 1-3 % slower on
+// every config: the extra live registers cost more occupancy than the overlap gave.)
+// L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
+// tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores).
+template <bool L4, int V>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -247,192 +607,68 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const uint32_t i = p0 + lane;
     const bool valid = i < n;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+    const SpanSrc spans{offsets, stride, frame_len, frames_bytes, n};
 
-    Frame fr = {0, 0};
-    if (valid) fr = frame_span(offsets, stride, frame_len, frames_bytes, i);
-    W.fo[lane] = fr.off;
-    W.fl[lane] = fr.len;
-    wave_sync();
-
-    // ---- 1. header windows -> LDS (chunk c = frame c/8, piece c%8) ----
+    // 1. header windows -> LDS
+    const Frame fr = spans.get(i);
     {
         u32x4 d[kWinChunks];
-#pragma unroll
-        for (int k = 0; k < kWinChunks; ++k) {
-            const uint32_t c = k * kWave + lane;
-            const uint32_t q = c / kWinChunks, j = c % kWinChunks;
-            const uint32_t qo = W.fo[q], ql = W.fl[q];
-            const uint32_t a = (qo & ~15u) + 16u * j;
-            d[k] = load16(rs, (a < qo + ql) ? a : frames_bytes, frames_bytes);
-        }
-#pragma unroll
-        for (int k = 0; k < kWinChunks; ++k)
-            *reinterpret_cast<u32x4*>(&W.win[(k * kWave + lane) * 16]) = d[k];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, frames_bytes, fr, lane, d, addr);
+        window_commit(W, rs, frames_bytes, d, addr, fix, lane);
     }
     wave_sync();
 
-    // ---- 2. lane-per-frame parse from LDS ----
-    const uint32_t ph = fr.off & 15u;                  // frame byte x at win[ph + x]
-    const uint8_t* wb = &W.win[lane * kWin];
-    const uint8_t* f = wb + ph;
-    auto b8 = [&](uint32_t o) -> uint32_t { return f[o]; };
-    auto be16 = [&](uint32_t o) -> uint32_t { return (b8(o) << 8) | b8(o + 1); };
-    auto le32 = [&](uint32_t o) -> uint32_t {
-        return b8(o) | (b8(o + 1) << 8) | (b8(o + 2) << 16) | (b8(o + 3) << 24);
-    };
-    auto be32 = [&](uint32_t o) -> uint32_t {
-        return (b8(o) << 24) | (b8(o + 1) << 16) | (b8(o + 2) << 8) | b8(o + 3);
-    };
-
-    uint32_t w[20];
+    // 2. lane-per-frame parse
+    LaneRec L;
+    if constexpr (V == 1) {                                       // ablation: window only
+        const uint32_t* ww = reinterpret_cast<const uint32_t*>(&W.win[lane * kSlot]);
+        uint32_t x = 0;
 #pragma unroll
-    for (int k = 0; k < 20; ++k) w[k] = 0;
-    uint32_t status = RPKT_S_OK, nvlan = 0;
-    const uint32_t len = fr.len;
-    uint32_t stream_s = 0, stream_e = 0;             // absolute L4 bytes past the window
-    uint32_t l4_part = 0, l4_start_abs = 0, pseudo = 0;
-    bool want_l4 = false;
-    w[19] = len;
-
-    if (!valid) {
-        status = RPKT_S_ETH_SHORT;
-    } else if (len < 14) {                             // ether/generated.rs:36
-        status = RPKT_S_ETH_SHORT;
+        for (int k = 0; k < kWin / 4; ++k) x ^= ww[k];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) L.w[k] = x + k;
+        L.status = 0;
     } else {
-        uint32_t et = be16(12);                         // ether/generated.rs:55-59
-        w[1] = le32(0);
-        w[2] = b8(4) | (b8(5) << 8) | (b8(6) << 16) | (b8(7) << 24);
-        w[3] = le32(8);
-        uint32_t cur = 14, rem = len - 14;              // payload(), :63-67
-        uint32_t tci0 = 0, tci1 = 0, vet0 = 0, vet1 = 0;
-        while ((et == 0x8100u || et == 0x88a8u) && nvlan < RPKT_MAX_VLAN) {
-            if (rem < 4) { status = RPKT_S_VLAN_SHORT; break; }   // vlan/generated.rs:34
-            uint32_t tci = be16(cur);
-            et = be16(cur + 2);
-            if (nvlan == 0) { tci0 = tci; vet0 = et; } else { tci1 = tci; vet1 = et; }
-            nvlan++;
-            cur += 4;
-            rem -= 4;
-        }
-        w[4] = tci0 | (tci1 << 16);
-        w[5] = vet0 | (vet1 << 16);
-        uint32_t eth_et = be16(12);
-        if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
-        if (status == RPKT_S_OK) {
-            // Ipv4::parse, ipv4/generated.rs:35-51
-            w[16] = cur;                                       // l3_off
-            if (rem < 20) {
-                status = RPKT_S_IP_SHORT;
-            } else {
-                const uint32_t b0 = b8(cur);
-                const uint32_t ihl4 = (b0 & 0xfu) * 4u;
-                const uint32_t tot = be16(cur + 2);
-                if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
-                else if (ihl4 > rem) status = RPKT_S_IP_IHL_GT_LEN;
-                else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
-                else if (tot > rem) status = RPKT_S_IP_TOT_GT_LEN;
-                if (status == RPKT_S_OK) {
-                    const uint32_t proto = b8(cur + 9);
-                    const uint32_t src = be32(cur + 12), dst = be32(cur + 16);
-                    w[6] = b0 | (b8(cur + 1) << 8) | (tot << 16);
-                    w[7] = be16(cur + 4) | (be16(cur + 6) << 16);
-                    w[8] = b8(cur + 8) | (proto << 8) | (be16(cur + 10) << 16);
-                    w[9] = src;
-                    w[10] = dst;
-                    uint32_t ip_sum = 0;
-                    if (flags & RPKT_F_IP_SUM)
-                        ip_sum = be_sum(lds_range_sum(wb, ph + cur, ph + cur + ihl4),
-                                        fr.off + cur);
-                    const uint32_t l4 = cur + ihl4;            // Ipv4::payload, :115-127
-                    const uint32_t l4rem = tot - ihl4;
-                    w[16] |= l4 << 16;
-                    w[17] = l4 | (l4rem << 16);
-                    w[18] = ip_sum;
-                    uint32_t l4len = 0;
-                    if (proto == 17u) {
-                        // Udp::parse, udp/generated.rs:31-42
-                        if (l4rem < 8) status = RPKT_S_UDP_SHORT;
-                        else {
-                            const uint32_t ulen = be16(l4 + 4);
-                            if (ulen < 8 || ulen > l4rem) status = RPKT_S_UDP_BAD_LEN;
-                            else {
-                                w[11] = be16(l4) | (be16(l4 + 2) << 16);
-                                w[14] = ulen;
-                                w[15] = be16(l4 + 6);
-                                w[17] = (l4 + 8) | ((ulen - 8) << 16);   // Udp::payload :66-76
-                                l4len = ulen;
-                            }
-                        }
-                    } else if (proto == 6u) {
-                        // Tcp::parse, tcp/generated.rs:34-45
-                        if (l4rem < 20) status = RPKT_S_TCP_SHORT;
-                        else {
-                            const uint32_t hl = (b8(l4 + 12) >> 4) * 4u;
-                            if (hl < 20 || hl > l4rem) status = RPKT_S_TCP_BAD_DOFF;
-                            else {
-                                w[11] = be16(l4) | (be16(l4 + 2) << 16);
-                                w[12] = be32(l4 + 4);
-                                w[13] = be32(l4 + 8);
-                                w[14] = be16(l4 + 12) | (be16(l4 + 14) << 16);
-                                w[15] = be16(l4 + 16) | (be16(l4 + 18) << 16);
-                                w[17] = (l4 + hl) | ((l4rem - hl) << 16);  // Tcp::payload
-                                l4len = l4rem;
-                            }
-                        }
-                    } else {
-                        status = RPKT_S_L4_OTHER;
-                    }
-                    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
-                        want_l4 = true;
-                        // pseudo header (smoltcp pseudo_header_v4): src, dst, proto, len
-                        pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) +
-                                 proto + l4len;
-                        const uint32_t win_end = kWin - ph;   // frame offset where LDS ends
-                        const uint32_t e = l4 + l4len;
-                        const uint32_t e_in = e < win_end ? e : win_end;
-                        l4_part = lds_range_sum(wb, ph + l4, ph + e_in);
-                        l4_start_abs = fr.off + l4;
-                        if (e > win_end) {
-                            stream_s = fr.off + win_end;
-                            stream_e = fr.off + e;
-                        }
-                    }
-                }
-            }
-        }
-        w[0] = status | (nvlan << 8) | (eth_et << 16);
+        parse_lane(W, lane, fr, valid, flags, L);
     }
-    if (!valid || len < 14) w[0] = status;
 
-    // ---- 3. flattened stream for L4 bytes beyond the window (uniform call) ----
-    if (flags & RPKT_F_L4_SUM) {
-        uint32_t sp = wave_stream_sum(rs, frames_bytes, stream_s, stream_e, W, lane);
-        if (want_l4) {
-            const uint32_t seg = be_sum(l4_part + sp, l4_start_abs);
-            w[18] |= fold16(pseudo + seg) << 16;
+    // 3. L4 bytes beyond the window: flattened chunk stream over the tile
+    if (L4 && V != 1) {
+        const uint32_t sp = wave_stream_sum(rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
+        if (L.want_l4) {
+            const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
+            L.w[18] |= fold16(L.pseudo + seg) << 16;
         }
     }
 
-    if (valid) {
-        u32x4* out = reinterpret_cast<u32x4*>(recs + i);
+    // 4. records (+ flow events)
+    if constexpr (V == 3) {                                       // ablation: 4 B per frame
+        uint32_t x = 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
-            out[k] = u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
-        if (flags & RPKT_F_FLOW_EV) {
-            uint64_t ev = len;
-            uint32_t bucket = n_buckets;
-            const uint32_t proto = (w[8] >> 8) & 0xffu;
-            const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
-            if (status == RPKT_S_OK)
-                bucket = flow_hash(w[9], w[10], w[11] & 0xffffu, w[11] >> 16, proto) % n_buckets;
-            ev |= (uint64_t)bucket << 32;
-            if (ip_parsed && (w[18] & 0xffffu) != 0xffffu) ev |= 1ull << 48;
-            if (status == RPKT_S_OK && (w[18] >> 16) != 0xffffu &&
-                !(proto == 17u && (w[15] & 0xffffu) == 0))
-                ev |= 1ull << 49;
-            flow_ev[i] = ev;
-        }
+        for (int k = 0; k < 20; ++k) x ^= L.w[k];
+        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+    } else {
+        store_records(W, lane, L.w, recs, p0, n);
+        if ((flags & RPKT_F_FLOW_EV) && valid) flow_ev[i] = flow_event(L, n_buckets);
     }
+}
+
+// Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
+// chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
+__global__ __launch_bounds__(256)
+void copy_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, u32x4* __restrict__ out,
+                     uint32_t out16) {
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t i = t;
+    for (; i + 3 * T < in16; i += 4 * T) {
+        u32x4 a = in[i], b = in[i + T], c = in[i + 2 * T], d = in[i + 3 * T];
+        acc ^= a ^ b ^ c ^ d;
+    }
+    for (; i < in16; i += T) acc ^= in[i];
+    for (uint32_t j = t; j < out16; j += T) out[j] = acc + j;
 }
 
 // ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
@@ -637,9 +873,36 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(parse_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
-                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen,
-                  b->n, flags, recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0> : parse_kernel<false, 0>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+
+// Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse
+// kernel and the streaming-copy roofline reference, for tools/ablate.py.
+int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs, int variant,
+                           void* stream) {
+    if (!b || !recs || b->n == 0) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    hipStream_t st = (hipStream_t)stream;
+#define RPKT_V(v)                                                                       \
+    launch((flags & RPKT_F_L4_SUM) ? parse_kernel<true, v> : parse_kernel<false, v>,   \
+           dim3(grid), dim3(per_block), 0, st, b->frames_dev, (uint32_t)b->frames_bytes,   \
+           b->offsets_dev, b->stride, flen, b->n, flags, recs, (uint64_t*)nullptr, 0u)
+    switch (variant) {
+        case 0: return RPKT_V(0);
+        case 1: return RPKT_V(1);
+        case 3: return RPKT_V(3);
+        case 10:
+            return launch(copy_ref_kernel, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        default: return RPKT_E_INVAL;
+    }
+#undef RPKT_V
 }
 
 size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets) {
