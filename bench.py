@@ -113,6 +113,21 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
     return wall, kern_ms
 
 
+def pmc_traffic(cfg):
+    """Per-launch HBM traffic of parse_kernel for this config from the rocprofv3 PMC
+    summary committed under profiles/ (tools/traffic.py), when it was measured on
+    this exact engine build; else None."""
+    path = os.path.join(ROOT, "profiles", "traffic_c%d.json" % cfg)
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("engine_build") != engine.lib().rpkt_gpu_build_info().decode():
+        return None, None
+    return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     """The CPU restatement of rpkt's path (oracle/, kind "port") timed on this host
     over a bounded sample of the same workload; also checks the GPU records of the
@@ -179,12 +194,13 @@ def run_config(cfg, args, rank, world, cpu=False):
     mpps = frames_step * world * args.steps / wall / 1e6
     gbps = bytes_step * world * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
+    traffic, tsrc = pmc_traffic(cfg)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
         "kernel_ms": kern_ms, "scaling": scaling, "frames_per_rank": int(frames_step),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": traffic, "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(alg_step)},
         "flags": FLAG_NAMES[flags], "layout": ("stride%d" % hbs[0].stride) if hbs[0].stride
         else "packed+u32 offsets",
@@ -258,6 +274,7 @@ def main():
                        if args.config != 4 else "shard x%d + RCCL all-reduce" % world},
             "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
             "kernel_ms": round(main_res["kernel_ms"], 5),
+            "engine_build": engine.lib().rpkt_gpu_build_info().decode(),
             "roofline": main_res["roofline"],
             "cpu_baseline": main_res.get("cpu_baseline"),
             "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)

@@ -28,11 +28,22 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_hash():
+    """Short hash of the engine sources: ties profiles/ numbers to a kernel build."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in GPU_SRC + HDR:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 def build_gpu(force=False, extra=()):
     os.makedirs(OUT, exist_ok=True)
     if force or _stale(GPU_LIB, GPU_SRC + HDR):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-o", GPU_LIB] + list(extra) + GPU_SRC
+               "-Wall", '-DRPKT_SRC_HASH="%s"' % source_hash(), "-o", GPU_LIB] + \
+            list(extra) + GPU_SRC
         subprocess.check_call(cmd)
     return GPU_LIB
 

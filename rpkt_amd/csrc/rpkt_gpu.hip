@@ -559,21 +559,29 @@ __device__ __forceinline__ uint64_t flow_event(const LaneRec& L, uint32_t n_buck
 }
 
 // Records of the tile staged through LDS (stride 21 dwords: conflict-free writes) and
-// stored as 5 wave-instructions of 1 KiB contiguous each.
+// stored as wave-instructions of 1 KiB contiguous each.  Record chunks [K0, K1) of the
+// 5 per record are stored (the L4 build stores chunks 0-3 before its stream phase
+// and chunk 4, which holds the sums, after it).
+template <int K0, int K1, bool NT>
 __device__ __forceinline__ void store_records(WaveScratch& W, int lane, const uint32_t (&w)[20],
                                               rpkt_rec_t* recs, uint32_t p0, uint32_t n) {
     wave_sync();
     uint32_t* rl = reinterpret_cast<uint32_t*>(W.win);
 #pragma unroll
-    for (int k = 0; k < 20; ++k) rl[lane * 21 + k] = w[k];
+    for (int k = 4 * K0; k < 4 * K1; ++k) rl[lane * 21 + k] = w[k];
     wave_sync();
     const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(recs + p0);
+    constexpr int kc = K1 - K0;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+    for (int k = 0; k < kc; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / kc, pc = K0 + c % kc;
         const uint32_t* src = rl + r * 21 + pc * 4;
-        if (r < nrec) out[c] = u32x4{src[0], src[1], src[2], src[3]};
+        const u32x4 v = {src[0], src[1], src[2], src[3]};
+        if (r < nrec) {
+            if constexpr (NT) __builtin_nontemporal_store(v, &out[r * 5 + pc]);
+            else out[r * 5 + pc] = v;
+        }
     }
 }
 
@@ -591,7 +599,8 @@ struct SpanSrc {
 // that prefetched the next tile's window into registers measured 1-3 % slower on
 // every config: the extra live registers cost more occupancy than the overlap gave.)
 // L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
-// tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores).
+// tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
+// 8 = plain instead of non-temporal record stores).
 template <bool L4, int V>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
@@ -633,6 +642,9 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         parse_lane(W, lane, fr, valid, flags, L);
     }
 
+    // Records leave with non-temporal stores (measured: -12 % at 64 B, -2 % at 1500 B
+    // vs plain stores); storing chunks 0-3 before the L4 stream measured 10-20 % slower.
+    constexpr bool kNT = (V != 8);
     // 3. L4 bytes beyond the window: flattened chunk stream over the tile
     if (L4 && V != 1) {
         const uint32_t sp = wave_stream_sum(rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
@@ -649,13 +661,15 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         for (int k = 0; k < 20; ++k) x ^= L.w[k];
         if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
     } else {
-        store_records(W, lane, L.w, recs, p0, n);
-        if ((flags & RPKT_F_FLOW_EV) && valid) flow_ev[i] = flow_event(L, n_buckets);
+        store_records<0, 5, kNT>(W, lane, L.w, recs, p0, n);
+        if ((flags & RPKT_F_FLOW_EV) && valid)
+            __builtin_nontemporal_store(flow_event(L, n_buckets), &flow_ev[i]);
     }
 }
 
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
 // chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
+template <int U, bool NT>
 __global__ __launch_bounds__(256)
 void copy_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, u32x4* __restrict__ out,
                      uint32_t out16) {
@@ -663,12 +677,18 @@ void copy_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, u32x4* __restr
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     u32x4 acc = {0u, 0u, 0u, 0u};
     uint32_t i = t;
-    for (; i + 3 * T < in16; i += 4 * T) {
-        u32x4 a = in[i], b = in[i + T], c = in[i + 2 * T], d = in[i + 3 * T];
-        acc ^= a ^ b ^ c ^ d;
+    for (; i + (U - 1) * T < in16; i += U * T) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = in[i + u * T];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= x[u];
     }
     for (; i < in16; i += T) acc ^= in[i];
-    for (uint32_t j = t; j < out16; j += T) out[j] = acc + j;
+    for (uint32_t j = t; j < out16; j += T) {
+        if constexpr (NT) __builtin_nontemporal_store(acc + j, &out[j]);
+        else out[j] = acc + j;
+    }
 }
 
 // ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
@@ -811,8 +831,11 @@ extern "C" {
 
 uint32_t rpkt_gpu_abi_version(void) { return RPKT_ABI_VERSION; }
 
+#ifndef RPKT_SRC_HASH
+#define RPKT_SRC_HASH "dev"
+#endif
 const char* rpkt_gpu_build_info(void) {
-    return "rpkt_gpu " __DATE__ " gfx950 hip; rec=80B; tile=64 frames/wave; win=128B";
+    return "rpkt_gpu src=" RPKT_SRC_HASH " gfx950; rec=80B; tile=64 frames/wave; win=128B";
 }
 
 const char* rpkt_gpu_status_name(int s) {
@@ -896,8 +919,21 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 0: return RPKT_V(0);
         case 1: return RPKT_V(1);
         case 3: return RPKT_V(3);
+        case 8: return RPKT_V(8);
         case 10:
-            return launch(copy_ref_kernel, dim3(2048), dim3(256), 0, st,
+            return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 11:
+            return launch(copy_ref_kernel<8, false>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 12:
+            return launch(copy_ref_kernel<8, true>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 13:
+            return launch(copy_ref_kernel<8, false>, dim3(8192), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
                           (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
         default: return RPKT_E_INVAL;

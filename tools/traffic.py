@@ -1,0 +1,57 @@
+"""Summarise a scripts/profile.sh run into profiles/: kernel durations and PMC HBM
+traffic per launch of the dominant kernel (parse_kernel).
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half of a
+wide coalesced streaming read (MI355X_MICROARCH.md §HBM), so the read side is
+doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+Usage: python tools/traffic.py <prof_dir> <config> <out_json>
+"""
+import csv
+import json
+import os
+import sys
+
+
+def rows(path):
+    with open(path) as fh:
+        return list(csv.DictReader(fh))
+
+
+def main(prof, cfg, out):
+    tr = [r for r in rows(os.path.join(prof, "trace_kernel_trace.csv"))
+          if r["Kernel_Name"].startswith("parse_kernel")]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr][5:]  # skip warmup
+    stats = rows(os.path.join(prof, "trace_kernel_stats.csv"))
+
+    def pmc(name):
+        v = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, name + "_counter_collection.csv"))
+             if r["Kernel_Name"].startswith("parse_kernel")][5:]
+        return sum(v) / len(v)
+
+    fetch_kib, write_kib = pmc("fetch"), pmc("write")
+    build = None
+    with open(os.path.join(prof, "trace_bench.log")) as fh:
+        for line in fh:
+            if line.startswith("{"):
+                build = json.loads(line).get("engine_build")
+    res = {
+        "config": cfg,
+        "engine_build": build,
+        "kernel": "parse_kernel",
+        "launches": len(durs),
+        "avg_duration_us": sum(durs) / len(durs) / 1e3,
+        "fetch_size_kib": fetch_kib,
+        "write_size_kib": write_kib,
+        "hbm_read_bytes_corrected": fetch_kib * 1024 * 2,
+        "hbm_write_bytes": write_kib * 1024,
+        "traffic_bytes_per_launch": fetch_kib * 1024 * 2 + write_kib * 1024,
+        "kernel_stats": stats,
+    }
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernel_stats"}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), sys.argv[3])
