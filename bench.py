@@ -30,7 +30,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from rpkt_amd import engine, gen  # noqa: E402
+from rpkt_amd import dist as rdist, engine, gen  # noqa: E402
 from rpkt_amd.records import REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
@@ -67,12 +67,15 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def algorithmic_bytes(hb):
-    """Bytes one launch must move: every frame byte read + the 80-B record written
-    (+ 4 B offset per frame for the packed layout).  SURVEY.md §8d."""
+def algorithmic_bytes(hb, flow=False):
+    """Bytes one step must move: every frame byte read + the 80-B record written
+    (+ 4 B offset per frame for the packed layout; + 8 B flow event written and read
+    back by the flow-counter pass).  SURVEY.md §8d."""
     b = int(hb.lens().sum()) + hb.n * REC_BYTES
     if hb.offsets is not None:
         b += 4 * (hb.n + 1)
+    if flow:
+        b += 16 * hb.n
     return b
 
 
@@ -128,11 +131,25 @@ def pmc_traffic(cfg):
     return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
 
 
+def head_sample(hb, max_bytes=256 << 20):
+    """The first frames of a host batch, at most ~max_bytes of frame data."""
+    lens = hb.lens()
+    m = int(np.searchsorted(np.cumsum(lens), max_bytes)) if lens.sum() > max_bytes else hb.n
+    m = max(1, min(m, hb.n))
+    if hb.offsets is not None:
+        offs = hb.offsets[:m + 1]
+        return gen.HostBatch(hb.config, m, hb.seed, hb.frames[:int(offs[-1])], offs, 0, 0)
+    return gen.HostBatch(hb.config, m, hb.seed, hb.frames[:m * hb.stride], None, hb.stride,
+                         hb.frame_len)
+
+
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     """The CPU restatement of rpkt's path (oracle/, kind "port") timed on this host
     over a bounded sample of the same workload; also checks the GPU records of the
     sample bit-exact against it."""
     from oracle import oracle
+    hb = head_sample(hb)
+    gpu_recs = gpu_recs[:hb.n]
     n = hb.n
     t0 = time.perf_counter()
     o = oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
@@ -154,7 +171,8 @@ def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     return {
         "value": round(frames_total / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
         "gb_per_s": round(bytes_total / dt / 1e9, 3),
-        "sample": "%d reps x %d frames of the same batch, 1 thread, %.1f s" % (reps, n, dt),
+        "sample": "%d reps x first %d frames (%.0f MB) of the batch, 1 thread, %.1f s" % (
+            reps, n, int(hb.lens().sum()) / 1e6, dt),
         "all_cores": {"threads": threads_all,
                       "value": round(n / dt_all / 1e6, 3), "unit": "Mpps"},
         "gpu_parity_on_sample": bool(parity),
@@ -166,7 +184,7 @@ def run_config(cfg, args, rank, world, cpu=False):
     flow = None
     if cfg == 4:                                   # strong scaling: shard one 8M batch
         n_total = args.frames or gen.DEFAULT_N[4]
-        lo, hi = n_total * rank // world, n_total * (rank + 1) // world
+        lo, hi = rdist.shard_range(n_total, rank, world)
         hbs = [gen.make_batch(4, hi - lo, first=lo)]
         scaling = "strong"
     else:                                          # weak scaling: a batch per rank
@@ -190,7 +208,7 @@ def run_config(cfg, args, rank, world, cpu=False):
 
     frames_step = sum(hb.n for hb in hbs) / len(hbs)
     bytes_step = sum(int(hb.lens().sum()) for hb in hbs) / len(hbs)
-    alg_step = sum(algorithmic_bytes(hb) for hb in hbs) / len(hbs)
+    alg_step = sum(algorithmic_bytes(hb, flow is not None) for hb in hbs) / len(hbs)
     mpps = frames_step * world * args.steps / wall / 1e6
     gbps = bytes_step * world * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
@@ -209,11 +227,10 @@ def run_config(cfg, args, rank, world, cpu=False):
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
-        if world > 1:
-            dist.all_reduce(flow["counters"], op=dist.ReduceOp.SUM)
+        rdist.reduce_counters(flow["counters"])         # RCCL all-reduce over xGMI
         torch.cuda.synchronize()
         red = time.perf_counter() - t0
-        c = flow["counters"].cpu().numpy().view(np.uint64).reshape(-1, 4)
+        c = rdist.counters_as_u64(flow["counters"])
         steps_run = args.steps + args.warmup
         out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
         out["flow_pkts_total"] = int(c[:, 0].sum())
@@ -232,18 +249,24 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--also", default="3", help="extra configs reported under 'extra'")
+    ap.add_argument("--also", default="3,4", help="extra configs reported under 'extra'")
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     rank, local, world = dist_env()
-    torch.cuda.set_device(local)
+    dev = local % torch.cuda.device_count() if args.dist_backend == "gloo" else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     want_cpu = (not args.no_cpu) and world == 1
 
     main_res = run_config(args.config, args, rank, world, cpu=want_cpu)

@@ -1,0 +1,63 @@
+"""world_size-2 gloo run of the multi-GPU logic on CPU: each rank generates only
+its shard of the IMIX batch (config 4), computes flow events + counters for it
+(the oracle stands in for the GPU here), and the counters are all-reduced; the
+result must equal the single-process counters of the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N = 60000
+NB = 8192
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    from rpkt_amd import dist as rd, gen
+    lo, hi = rd.shard_range(N, rank, world)
+    hb = gen.make_batch(4, hi - lo, first=lo)
+    _, ev = oracle.parse_batch(hb.frames, hb.n, flags=3, offsets=hb.offsets, n_buckets=NB,
+                               flow_ev=True)
+    c = torch.from_numpy(oracle.flow_count(ev, NB).view(np.int64).copy())
+    rd.reduce_counters(c)
+    if rank == 0:
+        np.save(out, c.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_counters_equal_whole_batch(tmp_path, world):
+    from oracle import oracle
+    from rpkt_amd import gen
+    out = str(tmp_path / "c.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out).view(np.uint64)
+    hb = gen.make_batch(4, N)
+    _, ev = oracle.parse_batch(hb.frames, hb.n, flags=3, offsets=hb.offsets, n_buckets=NB,
+                               flow_ev=True)
+    assert np.array_equal(got, oracle.flow_count(ev, NB))
+
+
+def test_shard_ranges_partition():
+    from rpkt_amd.dist import shard_range
+    for n in (0, 1, 7, 1000, 8 << 20):
+        for w in (1, 2, 3, 8):
+            r = [shard_range(n, k, w) for k in range(w)]
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(r[k][1] == r[k + 1][0] for k in range(w - 1))
+            assert max(b - a for a, b in r) - min(b - a for a, b in r) <= 1
