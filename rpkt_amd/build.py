@@ -57,8 +57,21 @@ def build_gen(force=False):
     return GEN_LIB
 
 
+EXAMPLE_SRC = os.path.join(ROOT, "examples", "parse_batch.cpp")
+EXAMPLE_BIN = os.path.join(ROOT, "examples", "parse_batch")
+
+
+def build_example(force=False):
+    """The C++ host example: links librpkt_gpu.so through the C ABI only."""
+    if force or _stale(EXAMPLE_BIN, [EXAMPLE_SRC, GPU_LIB] + HDR):
+        cmd = [HIPCC, "-O2", "-I" + os.path.join(ROOT, "include"), EXAMPLE_SRC, "-L" + OUT,
+               "-lrpkt_gpu", "-Wl,-rpath,$ORIGIN/../rpkt_amd/_build", "-o", EXAMPLE_BIN]
+        subprocess.check_call(cmd)
+    return EXAMPLE_BIN
+
+
 def build_all(force=False):
-    return build_gpu(force), build_gen(force)
+    return build_gpu(force), build_gen(force), build_example(force)
 
 
 if __name__ == "__main__":

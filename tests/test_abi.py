@@ -89,3 +89,8 @@ def test_engine_refuses_cpu_fallback():
         pytest.skip("GPU present")
     with pytest.raises(engine.RpktError):
         engine.alloc_records(4)
+
+
+def test_cpp_example_builds_against_header():
+    from rpkt_amd.build import build_example
+    assert os.path.exists(build_example())

@@ -207,3 +207,13 @@ def test_checksum_ranges_match_from_slice(torch):
     got = out.cpu().numpy().view(np.uint16)
     want = [oracle.from_slice(buf[s:s + l]) for s, l in ranges[:3000]]
     assert got[:3000].tolist() == want
+
+
+def test_cpp_host_example_through_c_abi(torch):
+    """examples/parse_batch: a non-Python host (plain hipMalloc) drives the C ABI."""
+    import subprocess
+    from rpkt_amd.build import build_example
+    exe = build_example()
+    r = subprocess.run([exe, "100000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "status=OK" in r.stdout and "sport=60376" in r.stdout
