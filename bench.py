@@ -79,7 +79,7 @@ def algorithmic_bytes(hb, flow=False):
     return b
 
 
-def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
+def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3):
     """Time `steps` launches (rotating over dbs).  Returns wall seconds (max over
     ranks) and the mean per-launch device time from two HIP events recorded on the
     launch stream around the back-to-back launches."""
@@ -97,8 +97,18 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
         else:
             engine.parse_batch(db, flags, recs=rc, stream=stream)
 
-    for k in range(warmup):
+    # W untimed warmup launches, extended to >= min_warm_s of GPU work: after the
+    # host-side batch generation the GPU sits idle and its clocks ramp back up over
+    # tens of ms (measured: 339 us/launch over 20 steps vs 299 over 200 at 1500 B)
+    k = 0
+    t_w = time.perf_counter()
+    while k < warmup or time.perf_counter() - t_w < min_warm_s:
         one(k)
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    warm_launches = k
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier(world)
@@ -113,7 +123,7 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None):
     barrier(world)
     wall = max_over_ranks(t1 - t0, world)
     kern_ms = ev0.elapsed_time(ev1) / steps      # back-to-back launches on `stream`
-    return wall, kern_ms
+    return wall, kern_ms, warm_launches
 
 
 def pmc_traffic(cfg):
@@ -204,7 +214,8 @@ def run_config(cfg, args, rank, world, cpu=False):
     torch.cuda.synchronize()
     log(rank, "config %d: %d frames/rank x %d batches resident, flags=%d" % (
         cfg, hbs[0].n, len(hbs), flags))
-    wall, kern_ms = time_parse(dbs, recs, flags, args.steps, args.warmup, world, flow)
+    wall, kern_ms, warm = time_parse(dbs, recs, flags, args.steps, args.warmup, world, flow,
+                                     args.min_warmup_s)
 
     frames_step = sum(hb.n for hb in hbs) / len(hbs)
     bytes_step = sum(int(hb.lens().sum()) for hb in hbs) / len(hbs)
@@ -215,6 +226,7 @@ def run_config(cfg, args, rank, world, cpu=False):
     traffic, tsrc = pmc_traffic(cfg)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
+        "warmup_launches": warm,
         "kernel_ms": kern_ms, "scaling": scaling, "frames_per_rank": int(frames_step),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -255,6 +267,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--min-warmup-s", type=float, default=0.3,
+                    help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
@@ -297,6 +311,7 @@ def main():
                        if args.config != 4 else "shard x%d + RCCL all-reduce" % world},
             "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
             "kernel_ms": round(main_res["kernel_ms"], 5),
+            "warmup_launches": main_res["warmup_launches"],
             "engine_build": engine.lib().rpkt_gpu_build_info().decode(),
             "roofline": main_res["roofline"],
             "cpu_baseline": main_res.get("cpu_baseline"),

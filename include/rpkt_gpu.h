@@ -198,6 +198,18 @@ int rpkt_gpu_checksum_ranges(const uint8_t* buf_dev, uint64_t buf_bytes,
                              const uint32_t* ranges_dev, uint32_t n,
                              uint16_t* out_dev, void* stream);
 
+/* Batched checksum::from_buf over multi-segment buffers (mbuf chains, rpkt-dpdk's
+ * Pbuf): chain p is segments chain_first_dev[p] .. chain_first_dev[p+1]-1 (n_chains+1
+ * entries), segment i = buf[segs_dev[2i] .. segs_dev[2i] + segs_dev[2i+1]).
+ * out_dev[p] = from_buf over the chain's bytes in order, pairing a segment's odd tail
+ * byte with the next segment's first byte.  Drop-in for rpkt/src/checksum.rs:8-27
+ * (with from_slice_with_tail_byte :77-111).  workspace_dev holds
+ * rpkt_gpu_checksum_chains_workspace_bytes(n_segs) bytes. */
+size_t rpkt_gpu_checksum_chains_workspace_bytes(uint32_t n_segs);
+int rpkt_gpu_checksum_chains(const uint8_t* buf_dev, uint64_t buf_bytes, const uint32_t* segs_dev,
+                             uint32_t n_segs, const uint32_t* chain_first_dev, uint32_t n_chains,
+                             uint16_t* out_dev, void* workspace_dev, void* stream);
+
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,
                         uint16_t dst_port, uint8_t protocol);

@@ -837,6 +837,53 @@ void checksum_ranges_kernel(const uint8_t* __restrict__ buf, uint32_t buf_bytes,
     if (i < n) out[i] = (uint16_t)be_sum(part, s);
 }
 
+// ---- batched checksum::from_buf over segment chains (mbuf chains) ----
+// Pass 1: every segment's standalone big-endian sum (the ranges kernel) plus its
+// length parity.  Pass 2: lane per chain folds its segments in order; a segment that
+// starts at an odd offset of the chain's byte stream contributes its byte-swapped
+// sum, which is exactly from_buf's pairing of a chunk's odd tail byte with the next
+// chunk's first byte (checksum.rs:13-24, 82-88).
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void segment_sums_kernel(const uint8_t* __restrict__ buf, uint32_t buf_bytes,
+                         const uint32_t* __restrict__ segs, uint32_t n,
+                         uint32_t* __restrict__ seg_out) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    uint32_t s = 0, e = 0, len = 0;
+    if (i < n) {
+        uint64_t st = segs[2 * i], ln = segs[2 * i + 1];
+        len = (uint32_t)ln;
+        if (st > buf_bytes) st = buf_bytes;
+        if (st + ln > buf_bytes) ln = buf_bytes - st;
+        s = (uint32_t)st;
+        e = (uint32_t)(st + ln);
+    }
+    const uint32_t part =
+        wave_stream_sum(make_rsrc(buf, buf_bytes), buf_bytes, s, e, scratch[wid], lane);
+    if (i < n) seg_out[i] = be_sum(part, s) | ((len & 1u) << 16);
+}
+
+__global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
+                                  const uint32_t* __restrict__ first, uint32_t n_chains,
+                                  uint32_t n_segs, uint16_t* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_chains) return;
+    uint32_t a = first[p], b = first[p + 1];
+    if (b > n_segs) b = n_segs;
+    uint32_t acc = 0, odd = 0;
+    for (uint32_t i = a; i < b; ++i) {
+        const uint32_t v = seg_out[i];
+        const uint32_t sum = v & 0xffffu;
+        acc += odd ? bswap16(sum) : sum;
+        odd ^= v >> 16;
+    }
+    out[p] = (uint16_t)fold16(acc);
+}
+
 thread_local int g_last_hip_error = 0;
 
 inline int hip_check(hipError_t e) {
@@ -1028,6 +1075,28 @@ int rpkt_gpu_checksum_ranges(const uint8_t* buf, uint64_t buf_bytes, const uint3
     const uint32_t per_block = kWave * kWavesPerBlock;
     return launch(checksum_ranges_kernel, dim3((n + per_block - 1) / per_block), dim3(per_block),
                   0, (hipStream_t)stream, buf, (uint32_t)buf_bytes, ranges, n, out);
+}
+
+size_t rpkt_gpu_checksum_chains_workspace_bytes(uint32_t n_segs) {
+    return (size_t)(n_segs ? n_segs : 1) * sizeof(uint32_t);
+}
+
+int rpkt_gpu_checksum_chains(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* segs,
+                             uint32_t n_segs, const uint32_t* chain_first, uint32_t n_chains,
+                             uint16_t* out, void* workspace, void* stream) {
+    if (n_chains == 0) return RPKT_OK;
+    if (!chain_first || !out || (n_segs && (!buf || !segs || !workspace))) return RPKT_E_INVAL;
+    if (buf_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    if (n_segs) {
+        int rc = launch(segment_sums_kernel, dim3((n_segs + per_block - 1) / per_block),
+                        dim3(per_block), 0, st, buf, (uint32_t)buf_bytes, segs, n_segs,
+                        (uint32_t*)workspace);
+        if (rc) return rc;
+    }
+    return launch(chain_fold_kernel, dim3((n_chains + 255) / 256), dim3(256), 0, st,
+                  (const uint32_t*)workspace, chain_first, n_chains, n_segs, out);
 }
 
 }  // extern "C"

@@ -31,7 +31,8 @@ class Batch(ctypes.Structure):
 
 EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
            "rpkt_gpu_last_hip_error", "rpkt_gpu_device_info", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
-           "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash"]
+           "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
+           "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains"]
 
 _lib = None
 
@@ -67,6 +68,12 @@ def lib():
         L.rpkt_gpu_checksum_ranges.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_checksum_ranges.restype = ctypes.c_int
+        L.rpkt_gpu_checksum_chains_workspace_bytes.argtypes = [ctypes.c_uint32]
+        L.rpkt_gpu_checksum_chains_workspace_bytes.restype = ctypes.c_size_t
+        L.rpkt_gpu_checksum_chains.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_checksum_chains.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -179,4 +186,21 @@ def checksum_ranges(buf, ranges, out=None, stream=None):
     rc = lib().rpkt_gpu_checksum_ranges(buf.data_ptr(), buf.numel(), ranges.data_ptr(), n,
                                         out.data_ptr(), _stream_ptr(stream))
     _check(rc, "rpkt_gpu_checksum_ranges")
+    return out
+
+
+def checksum_chains(buf, segs, chain_first, out=None, stream=None):
+    """rpkt_gpu_checksum_chains: batched checksum::from_buf over segment chains.
+    segs: int32 tensor of (start, len) pairs; chain_first: n_chains + 1 indices."""
+    torch = _torch()
+    n_segs = segs.numel() // 2
+    n_chains = chain_first.numel() - 1
+    if out is None:
+        out = torch.empty(max(n_chains, 0), dtype=torch.int16, device=buf.device)
+    ws = torch.empty(int(lib().rpkt_gpu_checksum_chains_workspace_bytes(n_segs)),
+                     dtype=torch.uint8, device=buf.device)
+    rc = lib().rpkt_gpu_checksum_chains(buf.data_ptr(), buf.numel(), segs.data_ptr(), n_segs,
+                                        chain_first.data_ptr(), n_chains, out.data_ptr(),
+                                        ws.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_checksum_chains")
     return out

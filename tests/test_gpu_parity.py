@@ -217,3 +217,26 @@ def test_cpp_host_example_through_c_abi(torch):
     r = subprocess.run([exe, "100000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "status=OK" in r.stdout and "sport=60376" in r.stdout
+
+
+def test_checksum_chains_match_from_buf(torch):
+    """Multi-segment (mbuf chain) sums vs the oracle's from_buf (checksum.rs:8-27):
+    segments of odd and even lengths at arbitrary buffer offsets, chains of 0..9."""
+    rng = np.random.default_rng(4)
+    buf = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
+    n_chains = 5000
+    counts = rng.integers(0, 10, n_chains)
+    first = np.zeros(n_chains + 1, dtype=np.uint32)
+    first[1:] = np.cumsum(counts)
+    n_segs = int(first[-1])
+    starts = rng.integers(0, buf.size - 3000, n_segs)
+    lens = rng.integers(0, 3000, n_segs)
+    lens[::7] = rng.integers(0, 3, (n_segs + 6) // 7)           # tiny segments
+    segs = np.stack([starts, lens], 1).astype(np.uint32)
+    out = engine.checksum_chains(torch.from_numpy(buf).cuda(),
+                                 torch.from_numpy(segs.view(np.int32)).cuda(),
+                                 torch.from_numpy(first.view(np.int32)).cuda())
+    got = out.cpu().numpy().view(np.uint16)
+    for p in range(0, n_chains, 3):
+        parts = [buf[s:s + l].tobytes() for s, l in segs[first[p]:first[p + 1]]]
+        assert got[p] == oracle.from_buf(parts), p
