@@ -149,6 +149,104 @@ class EtherFrame:
         return Cursor(b.rec, b.frame, "l3", 0, 14, b.length - 14)
 
 
+class EtherDot3Frame:
+    """IEEE 802.3 frame: the type field is a payload length (ether/generated.rs:137-200)."""
+
+    def __init__(self, buf):
+        self.buf, self.rec = buf, buf.rec
+
+    @staticmethod
+    def parse(buf):
+        """Err iff chunk_len < 14 or payload_len + 14 > remaining (ether/generated.rs:162-173)."""
+        rec = buf.rec
+        if buf.stage != "ether" or _st(rec) == STATUS["ETH_SHORT"]:
+            return Err(buf)
+        if int(rec["ethertype"]) + 14 > buf.length:
+            return Err(buf)
+        return Ok(EtherDot3Frame(buf))
+
+    def dst_addr(self):
+        return bytes(int(x) for x in self.rec["dst_addr"])
+
+    def src_addr(self):
+        return bytes(int(x) for x in self.rec["src_addr"])
+
+    def payload_len(self):
+        return int(self.rec["ethertype"])
+
+    def payload(self):
+        b = self.buf
+        return Cursor(b.rec, b.frame, "dot3", 0, 14, self.payload_len())
+
+
+class EtherGroup:
+    """EtherGroup::group_parse (ether/generated.rs:292-302): Ethernet II when the
+    type field is >= 1536, IEEE 802.3 when <= 1500, Err otherwise."""
+
+    @staticmethod
+    def group_parse(buf):
+        rec = buf.rec
+        if buf.stage != "ether" or _st(rec) == STATUS["ETH_SHORT"]:
+            return Err(buf)
+        v = int(rec["ethertype"])
+        if v >= 1536:
+            return EtherFrame.parse(buf)
+        if v <= 1500:
+            return EtherDot3Frame.parse(buf)
+        return Err(buf)
+
+
+class VlanDot3Frame:
+    """802.1Q tag whose type field is a payload length (vlan/generated.rs:153-205)."""
+
+    def __init__(self, buf):
+        self.buf, self.rec, self.i = buf, buf.rec, buf.vlan_idx
+
+    @staticmethod
+    def parse(buf):
+        rec = buf.rec
+        if buf.stage != "l3" or buf.vlan_idx >= int(rec["n_vlan"]):
+            return Err(buf)
+        if int(rec["vlan_ethertype"][buf.vlan_idx]) + 4 > buf.length:
+            return Err(buf)
+        return Ok(VlanDot3Frame(buf))
+
+    def _tci(self):
+        return int(self.rec["vlan_tci"][self.i])
+
+    def priority(self):
+        return self._tci() >> 13
+
+    def dei_flag(self):
+        return bool(self._tci() & 0x1000)
+
+    def vlan_id(self):
+        return self._tci() & 0xfff
+
+    def payload_len(self):
+        return int(self.rec["vlan_ethertype"][self.i])
+
+    def payload(self):
+        b = self.buf
+        return Cursor(b.rec, b.frame, "dot3", self.i + 1, b.off + 4, self.payload_len())
+
+
+class VlanGroup:
+    """VlanGroup::group_parse (vlan/generated.rs:312-322)."""
+
+    @staticmethod
+    def group_parse(buf):
+        rec = buf.rec
+        if buf.stage != "l3" or buf.vlan_idx >= int(rec["n_vlan"]):
+            return Err(buf)
+        v = int(rec["vlan_ethertype"][buf.vlan_idx])
+        if v >= 1536:
+            return VlanFrame.parse(buf)
+        if v <= 1500:
+            return VlanDot3Frame.parse(buf)
+        return Err(buf)
+
+
 class VlanFrame:
     def __init__(self, buf):
         self.buf, self.rec, self.i = buf, buf.rec, buf.vlan_idx
@@ -353,4 +451,5 @@ class Tcp(_L4):
 
 
 __all__ = ["EtherType", "IpProtocol", "Result", "Ok", "Err", "Cursor", "Packet",
-           "EtherFrame", "VlanFrame", "Ipv4", "Udp", "Tcp", "MAX_VLAN"]
+           "EtherFrame", "EtherDot3Frame", "EtherGroup", "VlanFrame", "VlanDot3Frame",
+           "VlanGroup", "Ipv4", "Udp", "Tcp", "MAX_VLAN"]

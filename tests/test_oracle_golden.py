@@ -184,3 +184,35 @@ def test_icmp_style_roundtrip():
         ck = (~oracle.from_slice(bytes(data))) & 0xffff
         data[2:4] = bytes([ck >> 8, ck & 0xff])
         assert oracle.from_slice(bytes(data)) == 0xffff
+
+
+def test_views_group_parse_dot3():
+    """rpkt/tests/eth_and_arp_test.rs:114-142: EtherGroup::group_parse -> EtherDot3Frame."""
+    from rpkt_amd.views import EtherGroup, EtherDot3Frame
+    frame = oracle.load_dat(os.path.join(PKTS, "EthDot3.dat"))
+    rec = oracle.parse_one(frame, flags=3)
+    d3 = EtherGroup.group_parse(Packet(rec, frame)).unwrap()
+    assert isinstance(d3, EtherDot3Frame)
+    assert d3.src_addr() == bytes.fromhex("0013f7115edb")
+    assert d3.dst_addr() == bytes.fromhex("0180c2000000")
+    assert d3.payload_len() == 38
+    llc = d3.payload().chunk()
+    assert llc[0] == 0x42 and llc[1] == 0x42 and llc[2] == 0x03   # BPDU dsap/ssap, control
+    assert len(llc) - 3 == 35
+    # an Ethernet II frame dispatches to EtherFrame
+    f2 = oracle.load_dat(os.path.join(PKTS, "bench_frame.dat"))
+    assert isinstance(EtherGroup.group_parse(Packet(oracle.parse_one(f2), f2)).unwrap(),
+                      EtherFrame)
+
+
+def test_views_vlan_group_parse_dot3():
+    """rpkt/tests/llc_test.rs:39-61: VlanGroup::group_parse -> VlanDot3Frame."""
+    from rpkt_amd.views import VlanGroup, VlanDot3Frame
+    frame = oracle.load_dat(os.path.join(PKTS, "llc_vlan.dat"))
+    rec = oracle.parse_one(frame, flags=3)
+    eth = EtherFrame.parse(Packet(rec, frame)).unwrap()
+    assert eth.ethertype() == EtherType.VLAN
+    vd = VlanGroup.group_parse(eth.payload()).unwrap()
+    assert isinstance(vd, VlanDot3Frame) and vd.payload_len() == 357
+    llc = vd.payload().chunk()
+    assert (llc[0], llc[1], llc[2]) == (0xaa, 0xaa, 0x03)
