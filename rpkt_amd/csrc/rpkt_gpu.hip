@@ -150,13 +150,21 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi) {
     return mh & ~ml;
 }
 
-__device__ __forceinline__ uint32_t halves(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// acc + low half + high half of w, in one v_dot2_u32_u16 against (1, 1)
+__device__ __forceinline__ uint32_t hsum(uint32_t w, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), u16x2{1, 1}, acc, false);
+}
+__device__ __forceinline__ uint32_t halves(uint32_t w) { return hsum(w, 0u); }
 
 // Word sum of bytes [lo, hi) of a 16-byte chunk (absolute phase).
 __device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
-    if (lo <= 0 && hi >= 16) return halves(d.x) + halves(d.y) + halves(d.z) + halves(d.w);
-    return halves(d.x & byte_mask(lo, hi)) + halves(d.y & byte_mask(lo - 4, hi - 4)) +
-           halves(d.z & byte_mask(lo - 8, hi - 8)) + halves(d.w & byte_mask(lo - 12, hi - 12));
+    if (lo <= 0 && hi >= 16) return hsum(d.w, hsum(d.z, hsum(d.y, hsum(d.x, 0u))));
+    uint32_t acc = hsum(d.x & byte_mask(lo, hi), 0u);
+    acc = hsum(d.y & byte_mask(lo - 4, hi - 4), acc);
+    acc = hsum(d.z & byte_mask(lo - 8, hi - 8), acc);
+    return hsum(d.w & byte_mask(lo - 12, hi - 12), acc);
 }
 
 // Flattened chunk stream over the tile: lane q owns absolute byte range
@@ -171,9 +179,14 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
 struct StreamBatch {
     u32x4 d[kStreamUnroll];
     uint32_t a[kStreamUnroll];       // chunk address
-    uint32_t q[kStreamUnroll];       // owning lane (range)
+    uint32_t m[kStreamUnroll];       // owner q | lo << 8 | hi << 13 | first << 18 | last << 19 |
+                                     // valid << 20 (lo, hi clipped to 0..16, chunk-relative)
 };
 
+// Resolve chunk c = base + u*64 + lane of the concatenated ranges: owner lane (the
+// ranges are in chunk order, so a lane's cursor only moves forward; binary search
+// only for jumps), address, and the clip/first/last metadata, so that consuming
+// the chunk needs no further LDS reads.
 template <int AUX>
 __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
                                              const WaveScratch& W, uint32_t total, uint32_t base,
@@ -181,9 +194,9 @@ __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t
 #pragma unroll
     for (int u = 0; u < kStreamUnroll; ++u) {
         const uint32_t c = base + u * kWave + lane;
-        // advance the lane's cursor to the range holding chunk c: ranges are in chunk
-        // order, so the cursor only moves forward; jump by binary search when far
-        if (W.pref[cur + 1] <= c) {
+        const bool valid = c < total;
+        uint32_t p1 = W.pref[cur + 1];
+        if (valid && p1 <= c) {
             if (W.pref[cur + 2] > c) {
                 cur += 1;
             } else {
@@ -193,34 +206,35 @@ __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t
                     if (W.pref[lo + step] <= c) lo += step;
                 cur = lo;
             }
+            p1 = W.pref[cur + 1];
         }
-        B.q[u] = cur;
-        B.a[u] = (W.s[cur] & ~15u) + 16u * (c - W.pref[cur]);
-        B.d[u] = load16_fast<AUX>(rs, c < total ? B.a[u] : oob);
+        const uint32_t q = cur, p0 = W.pref[q], sq = W.s[q], eq = W.e[q];
+        const uint32_t a = (sq & ~15u) + 16u * (c - p0);
+        const int lo = (int)sq - (int)a, hi = (int)eq - (int)a;
+        const uint32_t lo_c = lo < 0 ? 0u : (uint32_t)lo;                 // 0..15
+        const uint32_t hi_c = hi > 16 ? 16u : (hi < 0 ? 0u : (uint32_t)hi);
+        B.a[u] = a;
+        B.m[u] = q | (lo_c << 8) | (hi_c << 13) | ((uint32_t)(c == p0) << 18) |
+                 ((uint32_t)(c + 1 == p1) << 19) | ((uint32_t)valid << 20);
+        B.d[u] = load16_fast<AUX>(rs, valid ? a : oob);
     }
 }
 
 __device__ __forceinline__ void stream_consume(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
-                                               WaveScratch& W, uint32_t total, uint32_t base,
-                                               int lane, uint32_t& run, const StreamBatch& B) {
+                                               WaveScratch& W, int lane, uint32_t& run,
+                                               const StreamBatch& B) {
 #pragma unroll
     for (int u = 0; u < kStreamUnroll; ++u) {
-        const uint32_t c = base + u * kWave + lane;
-        uint32_t v = 0;
-        const uint32_t q = B.q[u];
-        if (c < total) {
-            const int lo = (int)W.s[q] - (int)B.a[u];
-            const int hi = (int)W.e[q] - (int)B.a[u];
-            v = chunk_sum(B.d[u], lo, hi);
-            if (__builtin_expect(straddles(B.a[u], oob), 0))    // buffer's last chunk
-                v = chunk_sum(load16(rs, B.a[u], oob), lo, hi);
-        }
+        const uint32_t m = B.m[u];
+        const int lo = (int)((m >> 8) & 31u), hi = (int)((m >> 13) & 31u);
+        uint32_t v = chunk_sum(B.d[u], lo, hi);                 // invalid lanes: d = 0
+        if (__builtin_expect((m >> 20) && straddles(B.a[u], oob), 0))   // buffer's last chunk
+            v = chunk_sum(load16(rs, B.a[u], oob), lo, hi);
         const uint32_t sc = wave_incl_scan(v) + run;
         run = __builtin_amdgcn_readlane(sc, 63);
-        if (c < total) {
-            if (c == W.pref[q]) W.first[q] = sc - v;
-            if (c + 1 == W.pref[q + 1]) W.last[q] = sc;
-        }
+        const uint32_t q = m & 63u;
+        if (m & (1u << 18)) W.first[q] = sc - v;
+        if (m & (1u << 19)) W.last[q] = sc;
     }
 }
 
@@ -247,10 +261,10 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
     stream_issue<AUX>(rs, oob, W, total, base, lane, cur, A);
     for (;;) {
         stream_issue<AUX>(rs, oob, W, total, base + kBatch, lane, cur, B);
-        stream_consume(rs, oob, W, total, base, lane, run, A);
+        stream_consume(rs, oob, W, lane, run, A);
         if (base + kBatch >= total) break;
         stream_issue<AUX>(rs, oob, W, total, base + 2 * kBatch, lane, cur, A);
-        stream_consume(rs, oob, W, total, base + kBatch, lane, run, B);
+        stream_consume(rs, oob, W, lane, run, B);
         if (base + 2 * kBatch >= total) break;
         base += 2 * kBatch;
     }
@@ -545,9 +559,10 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     }
 }
 
-// Flow event of a parsed frame (include/rpkt_gpu.h, rpkt_flow_ev_t).
-__device__ __forceinline__ uint64_t flow_event(const LaneRec& L, uint32_t n_buckets) {
-    const uint32_t* w = L.w;
+// Flow event of a parsed frame (include/rpkt_gpu.h, rpkt_flow_ev_t) from its record
+// words w (registers or the LDS stage).
+__device__ __forceinline__ uint64_t flow_event(const LaneRec& L, const uint32_t* w,
+                                               uint32_t n_buckets) {
     uint64_t ev = w[19];
     uint32_t bucket = n_buckets;
     const uint32_t proto = (w[8] >> 8) & 0xffu;
@@ -562,29 +577,37 @@ __device__ __forceinline__ uint64_t flow_event(const LaneRec& L, uint32_t n_buck
     return ev;
 }
 
-// Records of the tile staged through LDS (stride 21 dwords: conflict-free writes) and
-// stored as wave-instructions of 1 KiB contiguous each.  Record chunks [K0, K1) of the
-// 5 per record are stored (the L4 build stores chunks 0-3 before its stream phase
-// and chunk 4, which holds the sums, after it).
-template <int K0, int K1, bool NT>
-__device__ __forceinline__ void store_records(WaveScratch& W, int lane, const uint32_t (&w)[20],
-                                              rpkt_rec_t* recs, uint32_t p0, uint32_t n) {
-    wave_sync();
-    uint32_t* rl = reinterpret_cast<uint32_t*>(W.win);
+// Records of the tile are staged through LDS (the window area, free once the parse
+// is done; stride 21 dwords: conflict-free) and stored as wave-instructions of 1 KiB
+// contiguous each, with non-temporal stores (measured -12 % at 64 B, -2 % at 1500 B
+// vs plain).  Staging right after the parse keeps the 20 record words out of the
+// registers of the L4 stream.
+__device__ __forceinline__ uint32_t* rec_stage(WaveScratch& W) {
+    return reinterpret_cast<uint32_t*>(W.win);
+}
+
+__device__ __forceinline__ void stage_record(WaveScratch& W, int lane, const uint32_t (&w)[20]) {
+    wave_sync();                                     // every lane done reading the window
+    uint32_t* rl = rec_stage(W) + lane * 21;
 #pragma unroll
-    for (int k = 4 * K0; k < 4 * K1; ++k) rl[lane * 21 + k] = w[k];
+    for (int k = 0; k < 20; ++k) rl[k] = w[k];
+}
+
+template <bool NT>
+__device__ __forceinline__ void flush_records(WaveScratch& W, int lane, rpkt_rec_t* recs,
+                                              uint32_t p0, uint32_t n) {
     wave_sync();
+    const uint32_t* rl = rec_stage(W);
     const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(recs + p0);
-    constexpr int kc = K1 - K0;
 #pragma unroll
-    for (int k = 0; k < kc; ++k) {
-        const uint32_t c = k * kWave + lane, r = c / kc, pc = K0 + c % kc;
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
         const uint32_t* src = rl + r * 21 + pc * 4;
         const u32x4 v = {src[0], src[1], src[2], src[3]};
         if (r < nrec) {
-            if constexpr (NT) __builtin_nontemporal_store(v, &out[r * 5 + pc]);
-            else out[r * 5 + pc] = v;
+            if constexpr (NT) __builtin_nontemporal_store(v, &out[c]);
+            else out[c] = v;
         }
     }
 }
@@ -607,7 +630,7 @@ struct SpanSrc {
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
 // 22 = default-policy stream loads).
 template <bool L4, int V>
-__global__ __launch_bounds__(kWave * kWavesPerBlock)
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                   uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
@@ -647,9 +670,16 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         parse_lane(W, lane, fr, valid, flags, L);
     }
 
-    // Records leave with non-temporal stores (measured: -12 % at 64 B, -2 % at 1500 B
-    // vs plain stores); storing chunks 0-3 before the L4 stream measured 10-20 % slower.
-    constexpr bool kNT = (V != 8);
+    if constexpr (V == 3) {                                       // ablation: 4 B per frame
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 20; ++k) x ^= L.w[k];
+        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+        if (L4) wave_stream_sum<2>(rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
+        return;
+    }
+    stage_record(W, lane, L.w);
+
     // 3. L4 bytes beyond the window: flattened chunk stream over the tile
     if (L4 && V != 1) {
         // the L4 stream is read once: non-temporal loads (measured -13 % at 1500 B);
@@ -658,21 +688,16 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
             rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
         if (L.want_l4) {
             const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
-            L.w[18] |= fold16(L.pseudo + seg) << 16;
+            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
         }
     }
 
     // 4. records (+ flow events)
-    if constexpr (V == 3) {                                       // ablation: 4 B per frame
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < 20; ++k) x ^= L.w[k];
-        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
-    } else {
-        store_records<0, 5, kNT>(W, lane, L.w, recs, p0, n);
-        if ((flags & RPKT_F_FLOW_EV) && valid)
-            __builtin_nontemporal_store(flow_event(L, n_buckets), &flow_ev[i]);
+    if ((flags & RPKT_F_FLOW_EV) && valid) {
+        const uint64_t ev = flow_event(L, rec_stage(W) + lane * 21, n_buckets);
+        __builtin_nontemporal_store(ev, &flow_ev[i]);
     }
+    flush_records<V != 8>(W, lane, recs, p0, n);
 }
 
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
