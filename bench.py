@@ -67,6 +67,14 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def algorithmic_bytes(hb, flow=False):
     """Bytes one step must move: every frame byte read + the 80-B record written
     (+ 4 B offset per frame for the packed layout; + 8 B flow event written and read
@@ -243,10 +251,10 @@ def run_config(cfg, args, rank, world, cpu=False):
         torch.cuda.synchronize()
         red = time.perf_counter() - t0
         c = rdist.counters_as_u64(flow["counters"])
-        steps_run = args.steps + args.warmup
         out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
         out["flow_pkts_total"] = int(c[:, 0].sum())
-        out["flow_pkts_expected"] = int(n_total * steps_run)
+        # every launch (warmup included) added its shard's frames to the counters
+        out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
     if cpu and rank == 0:
         g = as_records(recs[0].cpu().numpy())
         out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds, args.cpu_threads)
