@@ -12,6 +12,8 @@ synthetic batch already resident in HBM.
             (reported under "extra").
   --config 4: 8,388,608-frame IMIX sharded over the ranks (strong scaling) with
             per-flow counters and one RCCL all-reduce of the counters.
+  --config 7: 262,144 x 8000 B jumbo frames as mbuf chains (2048-B segments in
+            shuffled 2176-B mempool slots), rpkt_gpu_parse_chains, full L3 + L4 sums.
 
 Multi-GPU: one process per GPU (torchrun); batches are independent, so ranks
 never exchange frames (weak scaling for configs 2/3).  The timed region is
@@ -39,7 +41,8 @@ FLAG_NAMES = {1: "ip_sum", 2: "l4_sum", 3: "ip_sum+l4_sum"}
 WORKLOAD = {2: "1M x 64B Ether/IPv4/UDP extract + IPv4 header checksum",
             3: "1M x 1500B Ether/IPv4/TCP parse + full L3/L4 checksum",
             4: "8M IMIX 64/570/1500 (7:4:1) TCP/UDP, sharded, flow counters + RCCL reduce",
-            5: "4M x U[64,1518]B 802.1Q/QinQ + IPv4 options -> TCP options"}
+            5: "4M x U[64,1518]B 802.1Q/QinQ + IPv4 options -> TCP options",
+            7: "256K x 8000B jumbo TCP/UDP as 2048-B mbuf chains, parse + full L3/L4 checksum"}
 
 
 def log(rank, *a):
@@ -80,6 +83,8 @@ def algorithmic_bytes(hb, flow=False):
     (+ 4 B offset per frame for the packed layout; + 8 B flow event written and read
     back by the flow-counter pass).  SURVEY.md §8d."""
     b = int(hb.lens().sum()) + hb.n * REC_BYTES
+    if isinstance(hb, gen.HostChains):             # segment descriptors + chain index
+        return b + 8 * hb.n_segs + 4 * (hb.n + 1)
     if hb.offsets is not None:
         b += 4 * (hb.n + 1)
     if flow:
@@ -102,6 +107,8 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
                                n_buckets=nb, stream=stream)
             engine.flow_count(flow["ev"][k % R], db.n, nb, counters=flow["counters"],
                               workspace=flow["ws"], stream=stream)
+        elif isinstance(db, engine.DeviceChains):
+            engine.parse_chains(db, flags, recs=rc, stream=stream)
         else:
             engine.parse_batch(db, flags, recs=rc, stream=stream)
 
@@ -161,6 +168,32 @@ def head_sample(hb, max_bytes=256 << 20):
                          hb.frame_len)
 
 
+def cpu_baseline_chains(hc, gpu_recs, flags, seconds, max_bytes=256 << 20):
+    """Chain oracle (oracle/rpkt_oracle_chain.c, 1 thread) over the first chains of
+    the batch (~max_bytes of frame data); checks the GPU records of the sample."""
+    from oracle import oracle
+    m = int(np.searchsorted(np.cumsum(hc.lens()), max_bytes))
+    m = max(1, min(m, hc.n))
+    first = hc.chain_first[:m + 1]
+    segs = hc.segs[:int(first[-1])]
+    t0 = time.perf_counter()
+    o = oracle.parse_chains(hc.buf, segs, first, flags)
+    one = time.perf_counter() - t0
+    reps = max(1, int(seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.parse_chains(hc.buf, segs, first, flags)
+    dt = time.perf_counter() - t0
+    nbytes = int(hc.lens()[:m].sum())
+    return {
+        "value": round(m * reps / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+        "gb_per_s": round(nbytes * reps / dt / 1e9, 3),
+        "sample": "%d reps x first %d chains (%.0f MB, %d segments) of the batch, 1 thread, "
+                  "%.1f s" % (reps, m, nbytes / 1e6, segs.shape[0], dt),
+        "gpu_parity_on_sample": bool(gpu_recs[:m].tobytes() == o.tobytes()),
+    }
+
+
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     """The CPU restatement of rpkt's path (oracle/, kind "port") timed on this host
     over a bounded sample of the same workload; also checks the GPU records of the
@@ -197,6 +230,13 @@ def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     }
 
 
+def layout_name(hb):
+    if isinstance(hb, gen.HostChains):
+        return "mbuf chains: %d segments of <= %d B, shuffled %d-B slots" % (
+            hb.n_segs, gen.MBUF_ROOM, gen.MBUF_ROOM + gen.MBUF_HEADROOM)
+    return ("stride%d" % hb.stride) if hb.stride else "packed+u32 offsets"
+
+
 def run_config(cfg, args, rank, world, cpu=False):
     flags = gen.FLAGS[cfg]
     flow = None
@@ -205,13 +245,18 @@ def run_config(cfg, args, rank, world, cpu=False):
         lo, hi = rdist.shard_range(n_total, rank, world)
         hbs = [gen.make_batch(4, hi - lo, first=lo)]
         scaling = "strong"
+    elif cfg in gen.CHAINED:                       # weak scaling: chains per rank
+        n = args.frames or gen.DEFAULT_N[cfg]
+        hbs = [gen.make_chains(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank)]
+        scaling = "weak"
     else:                                          # weak scaling: a batch per rank
         n = args.frames or gen.DEFAULT_N[cfg]
         R = args.rotate or (4 if cfg == 2 else 1)
         hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
                for r in range(R)]
         scaling = "weak"
-    dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
+    dbs = [engine.DeviceChains.from_host(hb) if cfg in gen.CHAINED else
+           engine.DeviceBatch.from_host(hb) for hb in hbs]
     recs = [engine.alloc_records(hb.n) for hb in hbs]
     if cfg == 4:
         nb = 8192
@@ -240,8 +285,7 @@ def run_config(cfg, args, rank, world, cpu=False):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(alg_step)},
-        "flags": FLAG_NAMES[flags], "layout": ("stride%d" % hbs[0].stride) if hbs[0].stride
-        else "packed+u32 offsets",
+        "flags": FLAG_NAMES[flags], "layout": layout_name(hbs[0]),
     }
     if cfg == 4:
         torch.cuda.synchronize()
@@ -257,7 +301,11 @@ def run_config(cfg, args, rank, world, cpu=False):
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
     if cpu and rank == 0:
         g = as_records(recs[0].cpu().numpy())
-        out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds, args.cpu_threads)
+        if cfg in gen.CHAINED:
+            out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds,
+                                               args.cpu_threads)
     del dbs, recs
     torch.cuda.empty_cache()
     return out
@@ -268,8 +316,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--also", default="3,4", help="extra configs reported under 'extra'")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 7])
+    ap.add_argument("--also", default="3,4,7", help="extra configs reported under 'extra'")
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -298,7 +346,7 @@ def main():
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
 
     if rank == 0:
-        fb = {2: 64, 3: 1500}.get(args.config)
+        fb = {2: 64, 3: 1500, 7: 8000}.get(args.config)
         line = {
             "metric": METRIC,
             "value": round(main_res["mpps"], 2),

@@ -210,6 +210,32 @@ int rpkt_gpu_checksum_chains(const uint8_t* buf_dev, uint64_t buf_bytes, const u
                              uint32_t n_segs, const uint32_t* chain_first_dev, uint32_t n_chains,
                              uint16_t* out_dev, void* workspace_dev, void* stream);
 
+/* Mbuf-chain batch (rpkt-dpdk's Mbuf segments read through a Pbuf,
+ * rpkt-dpdk/src/pbuf.rs).  Segment k = buf_dev[segs_dev[2k] .. segs_dev[2k] +
+ * segs_dev[2k+1]) (data offset, data_len; clamped to buf_bytes like frames; segs_dev
+ * 8-byte aligned).  Chain p = segments [a, b) with a = min(chain_first_dev[p], n_segs),
+ * b = min(max(chain_first_dev[p+1], a), n_segs) (n_chains + 1 entries); its pkt_len is
+ * the sum of its segments' lengths.  buf_bytes < 4 GiB, n_segs < 2^31. */
+typedef struct rpkt_chains {
+    const uint8_t*  buf_dev;
+    uint64_t        buf_bytes;
+    const uint32_t* segs_dev;
+    const uint32_t* chain_first_dev;
+    uint32_t        n_segs;
+    uint32_t        n_chains;
+} rpkt_chains_t;
+
+/* Parse + verify mbuf chains: rpkt_gpu_parse_batch's chain and record per chain, with
+ * each view's tests taken as they are over a Pbuf: header sizes against chunk() (the
+ * rest of the segment holding the header's first byte; Pbuf::new starts at segment 0
+ * even when it is empty), totals against remaining(), the packet end cut by the
+ * IPv4/UDP trim_off.  Record offsets are logical positions in the chain's bytes,
+ * frame_len = pkt_len, l4_sum = from_buf over the segments (rpkt/src/checksum.rs:8-27).
+ * The caller's segments are never modified (the reference's trim_off truncates the
+ * mbuf chain, mbuf.rs:346-382).  recs_dev n_chains * 80 B, 16-byte aligned. */
+int rpkt_gpu_parse_chains(const rpkt_chains_t* chains, uint32_t flags, rpkt_rec_t* recs_dev,
+                          rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
+
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,
                         uint16_t dst_port, uint8_t protocol);

@@ -55,6 +55,14 @@ def lib():
                                        ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
                                        ctypes.c_uint16]
         L.oracle_packet_l4.restype = ctypes.c_int
+        L.oracle_parse_chains.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_void_p]
+        L.oracle_parse_chains.restype = None
+        L.oracle_pbuf_script.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_pbuf_script.restype = None
         _lib = L
     return _lib
 
@@ -106,6 +114,33 @@ def parse_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0, n_bucke
         lib().oracle_parse_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
                                  flags, n_buckets, _ptr(recs), _ptr(ev))
     return (recs, ev) if flow_ev else recs
+
+
+def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False):
+    """Oracle records for mbuf chains (rpkt_gpu_parse_chains arguments, host memory):
+    segs = u32 (offset, length) pairs into buf, chain_first = n_chains + 1 entries."""
+    from rpkt_amd.records import REC_DTYPE
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    segs = np.ascontiguousarray(segs, dtype=np.uint32).reshape(-1)
+    cf = np.ascontiguousarray(chain_first, dtype=np.uint32)
+    n = cf.size - 1
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    ev = np.zeros(n, dtype=np.uint64) if flow_ev else None
+    lib().oracle_parse_chains(_ptr(buf), buf.size, _ptr(segs), segs.size // 2, _ptr(cf), n,
+                              flags, n_buckets, _ptr(recs), _ptr(ev))
+    return (recs, ev) if flow_ev else recs
+
+
+def pbuf_script(seg_lens, ops):
+    """Replay Pbuf operations [('new'|'advance'|'trim_off', count)] over segments of
+    the given lengths; returns one dict of the observable state per op."""
+    kinds = {"new": 0, "advance": 1, "trim_off": 2}
+    sl = np.ascontiguousarray(seg_lens, dtype=np.uint32)
+    o = np.array([[kinds[k], c] for k, c in ops], dtype=np.uint64).reshape(-1)
+    out = np.zeros(6 * len(ops), dtype=np.uint64)
+    lib().oracle_pbuf_script(_ptr(sl), sl.size, _ptr(o), len(ops), _ptr(out))
+    keys = ("cursor", "chunk_len", "remaining", "headroom", "num_segs", "pkt_len")
+    return [dict(zip(keys, (int(x) for x in out[6 * i:6 * i + 6]))) for i in range(len(ops))]
 
 
 def flow_count(ev, n_buckets):

@@ -26,7 +26,7 @@
 /* ------------------------------------------------------------------------- */
 
 /* propagate_carries, rpkt/src/checksum.rs:115-118 */
-static uint16_t propagate_carries(uint32_t word) {
+uint16_t oracle_propagate_carries(uint32_t word) {
     uint32_t sum = (word >> 16) + (word & 0xffff);
     return (uint16_t)((uint16_t)(sum >> 16) + (uint16_t)sum);
 }
@@ -54,19 +54,19 @@ uint16_t oracle_from_slice(const uint8_t* data, size_t len) {
     if (len == 1) {                                   /* :57-59 */
         accum += (uint32_t)data[0] << 8;
     }
-    return propagate_carries(accum);                  /* :61 */
+    return oracle_propagate_carries(accum);                  /* :61 */
 }
 
 /* combine, rpkt/src/checksum.rs:68-74 */
 uint16_t oracle_combine(const uint16_t* checksums, size_t n) {
     uint32_t accum = 0;
     for (size_t i = 0; i < n; i++) accum += checksums[i];
-    return propagate_carries(accum);
+    return oracle_propagate_carries(accum);
 }
 
 /* from_slice_with_tail_byte, rpkt/src/checksum.rs:77-111.
  * tail_in < 0 means None.  Returns the new tail byte or -1 (None). */
-static int from_slice_with_tail_byte(const uint8_t* data, size_t len, uint32_t* accum,
+int oracle_from_slice_with_tail_byte(const uint8_t* data, size_t len, uint32_t* accum,
                                      int tail_in) {
     if (tail_in >= 0) {                               /* :82-88 */
         *accum += ((uint32_t)(uint8_t)tail_in << 8) | data[0];
@@ -97,11 +97,11 @@ uint16_t oracle_from_buf(const uint8_t* const* segs, const size_t* seg_lens, siz
     for (size_t s = 0; s < n_segs && len > 0; s++) {  /* :13-20 */
         size_t cl = seg_lens[s] < len ? seg_lens[s] : len;
         if (cl == 0) continue;
-        tail = from_slice_with_tail_byte(segs[s], cl, &accum, tail);
+        tail = oracle_from_slice_with_tail_byte(segs[s], cl, &accum, tail);
         len -= cl;
     }
     if (tail >= 0) accum += (uint32_t)tail << 8;      /* :22-24 */
-    return propagate_carries(accum);
+    return oracle_propagate_carries(accum);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -134,7 +134,7 @@ static uint32_t be32(const uint8_t* p) {
 /* smoltcp pseudo_header_v4 as used by the verify composition:
  * combine(&[data(src), data(dst), data(&[0, proto, len_hi, len_lo])]).
  * smoltcp is the documented origin of checksum.rs (rpkt/src/checksum.rs:3). */
-static uint16_t pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
+uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
                                  uint16_t length) {
     uint8_t proto_len[4] = {0, proto, (uint8_t)(length >> 8), (uint8_t)length};
     uint16_t parts[3] = {oracle_from_slice(src4, 4), oracle_from_slice(dst4, 4),
@@ -224,7 +224,7 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
         rec->l4_word6 = (uint16_t)ulen;
         rec->l4_checksum = be16(u + 6);               /* :56-58 */
         if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {pseudo_header_v4(ip + 12, ip + 16, 17, (uint16_t)ulen),
+            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 17, (uint16_t)ulen),
                                  oracle_from_slice(u, ulen)};
             rec->l4_sum = oracle_combine(parts, 2);
         }
@@ -251,7 +251,7 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
         rec->l4_checksum = be16(t + 16);              /* :111-114 */
         rec->tcp_urgent = be16(t + 18);               /* :115-118 */
         if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {pseudo_header_v4(ip + 12, ip + 16, 6, (uint16_t)cl),
+            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 6, (uint16_t)cl),
                                  oracle_from_slice(t, cl)};
             rec->l4_sum = oracle_combine(parts, 2);
         }

@@ -1,0 +1,360 @@
+/*
+ * rpkt_oracle_chain.c — CPU restatement of rpkt's parse chain over a multi-segment
+ * packet buffer (rpkt-dpdk's Pbuf over an mbuf chain).  TEST INFRASTRUCTURE ONLY:
+ * tests/ and bench.py's cpu_baseline leg load it as the checker; the product path
+ * (librpkt_gpu.so) never links or calls it.
+ *
+ * Pbuf is restated field for field (rpkt-dpdk/src/pbuf.rs:8-16): the current
+ * segment, the chunk [chunk_start, chunk_start + chunk_len) inside it and segs_len,
+ * the bytes of all segments up to and including the current one.  The mbuf chain
+ * is the caller's segment list; Mbuf::truncate_to (rpkt-dpdk/src/mbuf.rs:346-382),
+ * which Pbuf::trim_off calls, is applied to a private copy of the segment lengths,
+ * so the caller's list is never modified.  The walker is pinned by the assertions
+ * of rpkt-dpdk/tests/pbuf.rs, replayed through oracle_pbuf_script
+ * (tests/test_oracle_chain.py).
+ *
+ * The header views (EtherFrame/VlanFrame/Ipv4/Udp/Tcp ::parse) are generic over
+ * `T: Buf` and test header lengths against `chunk().len()` and total lengths
+ * against `remaining()`; over a Pbuf those differ, which is the whole point of this
+ * file.  Lengths are 64-bit here (pkt_len is u32 and data_len u16 in DPDK).
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <stdlib.h>
+#include <stdio.h>
+
+#include "../include/rpkt_gpu.h"
+
+uint16_t oracle_from_slice(const uint8_t* data, size_t len);
+uint16_t oracle_combine(const uint16_t* checksums, size_t n);
+uint16_t oracle_propagate_carries(uint32_t word);
+int oracle_from_slice_with_tail_byte(const uint8_t* data, size_t len, uint32_t* accum,
+                                     int tail_in);
+uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
+                                 uint16_t length);
+uint64_t oracle_flow_event(const rpkt_rec_t* r, uint32_t n_buckets);
+
+/* ------------------------------------------------------------------------- */
+/* The mbuf chain and Pbuf                                                    */
+/* ------------------------------------------------------------------------- */
+
+typedef struct mchain {
+    const uint8_t* base;     /* arena holding every segment */
+    uint64_t* off;           /* data_addr of segment k, as an arena offset */
+    uint64_t* len;           /* data_len of segment k (mutable: truncate_to) */
+    uint32_t nb_segs;        /* segments still linked (seg k->next == NULL iff k+1 == nb_segs) */
+    uint64_t pkt_len;        /* Mbuf::pkt_len, mbuf.rs:250-252 */
+} mchain_t;
+
+typedef struct pbuf {
+    mchain_t* m;             /* mbuf_head */
+    uint32_t cur;            /* mbuf_cur */
+    uint64_t chunk_start;    /* arena offset */
+    uint64_t chunk_len;
+    uint64_t segs_len;
+} pbuf_t;
+
+static void die(const char* what) {
+    fprintf(stderr, "oracle: %s (the reference panics here)\n", what);
+    abort();
+}
+
+static int has_next(const pbuf_t* p) { return p->cur + 1 < p->m->nb_segs; }
+
+/* Pbuf::new, pbuf.rs:19-34 */
+static void pbuf_new(pbuf_t* p, mchain_t* m) {
+    p->m = m;
+    p->cur = 0;
+    p->chunk_len = m->nb_segs ? m->len[0] : 0;
+    p->chunk_start = m->nb_segs ? m->off[0] : 0;
+    p->segs_len = p->chunk_len;
+}
+
+/* Pbuf::cursor, pbuf.rs:41-44 */
+static uint64_t pbuf_cursor(const pbuf_t* p) { return p->segs_len - p->chunk_len; }
+
+/* Pbuf::advance_common, pbuf.rs:48-57 */
+static void pbuf_advance_common(pbuf_t* p, uint64_t target) {
+    while (p->segs_len <= target && has_next(p)) {
+        p->cur += 1;
+        p->segs_len += p->m->len[p->cur];
+    }
+    p->chunk_len = p->segs_len - target;
+    p->chunk_start = p->m->off[p->cur] + p->m->len[p->cur] - p->chunk_len;
+}
+
+/* Buf::remaining, pbuf.rs:98-101 */
+static uint64_t pbuf_remaining(const pbuf_t* p) { return p->m->pkt_len - pbuf_cursor(p); }
+
+/* Buf::advance, pbuf.rs:86-96 (slow path :59-64) */
+static void pbuf_advance(pbuf_t* p, uint64_t cnt) {
+    if (cnt >= p->chunk_len) {
+        if (cnt > pbuf_remaining(p)) die("advance past end");
+        pbuf_advance_common(p, pbuf_cursor(p) + cnt);
+    } else {
+        p->chunk_start += cnt;
+        p->chunk_len -= cnt;
+    }
+}
+
+/* PktBufMut::chunk_headroom, pbuf.rs:146-149 */
+static uint64_t pbuf_headroom(const pbuf_t* p) { return p->m->len[p->cur] - p->chunk_len; }
+
+/* Mbuf::truncate_to, mbuf.rs:346-382 */
+static void mbuf_truncate_to(mchain_t* m, uint64_t new_size) {
+    if (new_size > m->pkt_len) die("truncate_to past pkt_len");
+    uint32_t cur = 0;
+    uint64_t remaining = new_size;
+    while (m->len[cur] < remaining) {
+        remaining -= m->len[cur];
+        cur += 1;
+    }
+    if (cur + 1 < m->nb_segs) m->nb_segs = cur + 1;   /* free the trailing segments */
+    m->len[cur] = remaining;
+    m->pkt_len = new_size;
+}
+
+/* PktBuf::trim_off, pbuf.rs:117-140 */
+static void pbuf_trim_off(pbuf_t* p, uint64_t cnt) {
+    uint64_t cursor = pbuf_cursor(p);
+    if (cnt > pbuf_remaining(p)) die("trim_off past end");
+    uint64_t new_len = p->m->pkt_len - cnt;
+    if (cursor == new_len && pbuf_headroom(p) == 0) {
+        mbuf_truncate_to(p->m, new_len);
+        p->cur = 0;
+        p->segs_len = p->m->len[0];
+        pbuf_advance_common(p, cursor);
+    } else {
+        mbuf_truncate_to(p->m, new_len);
+        if (new_len < p->segs_len) {
+            p->chunk_len = new_len - cursor;
+            p->segs_len = new_len;
+        }
+    }
+}
+
+static const uint8_t* pbuf_chunk(const pbuf_t* p) { return p->m->base + p->chunk_start; }
+
+/* checksum::from_buf(buf, len), rpkt/src/checksum.rs:8-27, over a Pbuf (Buf::take) */
+static uint16_t pbuf_from_buf(pbuf_t buf, uint64_t len) {
+    uint32_t accum = 0;
+    int tail = -1;
+    uint64_t limit = len < pbuf_remaining(&buf) ? len : pbuf_remaining(&buf);
+    while (limit > 0) {                                /* has_remaining, :13 */
+        uint64_t cl = buf.chunk_len < limit ? buf.chunk_len : limit;
+        if (cl == 0 && tail >= 0) die("from_slice_with_tail_byte on an empty chunk");
+        if (cl) tail = oracle_from_slice_with_tail_byte(pbuf_chunk(&buf), cl, &accum, tail);
+        pbuf_advance(&buf, cl);                        /* :19 */
+        limit -= cl;
+    }
+    if (tail >= 0) accum += (uint32_t)tail << 8;       /* :22-24 */
+    return oracle_propagate_carries(accum);
+}
+
+static uint16_t be16(const uint8_t* p) { return (uint16_t)(((uint16_t)p[0] << 8) | p[1]); }
+static uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* ------------------------------------------------------------------------- */
+/* The decode chain over a Pbuf                                               */
+/* ------------------------------------------------------------------------- */
+
+/* Same chain and record as oracle_parse_one (rpkt_oracle.c), with every length
+ * test taken exactly as the generic views take it: header sizes against
+ * chunk().len(), IPv4/UDP totals against remaining(). */
+static void parse_pbuf(mchain_t* m, uint32_t flags, rpkt_rec_t* rec) {
+    memset(rec, 0, sizeof(*rec));
+    rec->frame_len = m->pkt_len > 0xffffffffull ? 0xffffffffu : (uint32_t)m->pkt_len;
+    pbuf_t buf;
+    pbuf_new(&buf, m);
+
+    /* EtherFrame::parse, ether/generated.rs:34-41 */
+    if (buf.chunk_len < 14) { rec->status = RPKT_S_ETH_SHORT; return; }
+    const uint8_t* e = pbuf_chunk(&buf);
+    memcpy(rec->dst_addr, e + 0, 6);
+    memcpy(rec->src_addr, e + 6, 6);
+    uint16_t et = be16(e + 12);
+    rec->ethertype = et;
+    pbuf_advance(&buf, 14);                           /* payload :63-67 */
+
+    /* VLAN walk, vlan/generated.rs:32-39 (chunk_len >= 4), payload :65-69 */
+    while ((et == 0x8100 || et == 0x88a8) && rec->n_vlan < RPKT_MAX_VLAN) {
+        if (buf.chunk_len < 4) { rec->status = RPKT_S_VLAN_SHORT; return; }
+        const uint8_t* v = pbuf_chunk(&buf);
+        rec->vlan_tci[rec->n_vlan] = be16(v);
+        et = be16(v + 2);
+        rec->vlan_ethertype[rec->n_vlan] = et;
+        rec->n_vlan++;
+        pbuf_advance(&buf, 4);
+    }
+    if (et != 0x0800) { rec->status = RPKT_S_NOT_IPV4; return; }
+
+    /* Ipv4::parse, ipv4/generated.rs:35-51 */
+    rec->l3_off = (uint16_t)pbuf_cursor(&buf);
+    uint64_t chunk_len = buf.chunk_len;
+    if (chunk_len < 20) { rec->status = RPKT_S_IP_SHORT; return; }
+    uint8_t ip[60];                                   /* the header lies inside the chunk */
+    memcpy(ip, pbuf_chunk(&buf), 20);
+    uint64_t header_len = (uint64_t)(ip[0] & 0xf) * 4;
+    uint64_t packet_len = be16(ip + 2);
+    if (header_len < 20) { rec->status = RPKT_S_IP_BAD_IHL; return; }
+    if (header_len > chunk_len) { rec->status = RPKT_S_IP_IHL_GT_LEN; return; }
+    if (packet_len < header_len) { rec->status = RPKT_S_IP_TOT_LT_IHL; return; }
+    if (packet_len > pbuf_remaining(&buf)) { rec->status = RPKT_S_IP_TOT_GT_LEN; return; }
+    memcpy(ip, pbuf_chunk(&buf), header_len);
+    rec->ip_vhl = ip[0];
+    rec->ip_tos = ip[1];
+    rec->ip_packet_len = (uint16_t)packet_len;
+    rec->ip_ident = be16(ip + 4);
+    rec->ip_frag = be16(ip + 6);
+    rec->ip_ttl = ip[8];
+    rec->ip_protocol = ip[9];
+    rec->ip_checksum = be16(ip + 10);
+    rec->ip_src = be32(ip + 12);
+    rec->ip_dst = be32(ip + 16);
+    if (flags & RPKT_F_IP_SUM) rec->ip_sum = oracle_from_slice(ip, header_len);
+
+    /* Ipv4::payload, ipv4/generated.rs:115-127 */
+    uint64_t trim_size = pbuf_remaining(&buf) - packet_len;
+    if (trim_size > 0) pbuf_trim_off(&buf, trim_size);
+    pbuf_advance(&buf, header_len);
+    rec->l4_off = (uint16_t)pbuf_cursor(&buf);
+    rec->payload_off = rec->l4_off;
+    rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+
+    uint8_t proto = ip[9];
+    if (proto == 17) {
+        /* Udp::parse, udp/generated.rs:31-42 */
+        if (buf.chunk_len < 8) { rec->status = RPKT_S_UDP_SHORT; return; }
+        const uint8_t* u = pbuf_chunk(&buf);
+        uint64_t ulen = be16(u + 4);
+        if (ulen < 8 || ulen > pbuf_remaining(&buf)) { rec->status = RPKT_S_UDP_BAD_LEN; return; }
+        rec->src_port = be16(u);
+        rec->dst_port = be16(u + 2);
+        rec->l4_word6 = (uint16_t)ulen;
+        rec->l4_checksum = be16(u + 6);
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 17, (uint16_t)ulen),
+                                 pbuf_from_buf(buf, ulen)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        /* Udp::payload, udp/generated.rs:66-76 */
+        uint64_t ts = pbuf_remaining(&buf) - ulen;
+        if (ts > 0) pbuf_trim_off(&buf, ts);
+        pbuf_advance(&buf, 8);
+        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
+        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+        rec->status = RPKT_S_OK;
+    } else if (proto == 6) {
+        /* Tcp::parse, tcp/generated.rs:34-45 */
+        uint64_t cl = buf.chunk_len;
+        if (cl < 20) { rec->status = RPKT_S_TCP_SHORT; return; }
+        const uint8_t* t = pbuf_chunk(&buf);
+        uint64_t hl = (uint64_t)(t[12] >> 4) * 4;
+        if (hl < 20 || hl > cl) { rec->status = RPKT_S_TCP_BAD_DOFF; return; }
+        rec->src_port = be16(t);
+        rec->dst_port = be16(t + 2);
+        rec->tcp_seq = be32(t + 4);
+        rec->tcp_ack = be32(t + 8);
+        rec->l4_word6 = be16(t + 12);
+        rec->tcp_window = be16(t + 14);
+        rec->l4_checksum = be16(t + 16);
+        rec->tcp_urgent = be16(t + 18);
+        uint64_t l4len = pbuf_remaining(&buf);        /* TCP length comes from IPv4 */
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 6, (uint16_t)l4len),
+                                 pbuf_from_buf(buf, l4len)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        pbuf_advance(&buf, hl);                       /* Tcp::payload :125-131 */
+        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
+        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+        rec->status = RPKT_S_OK;
+    } else {
+        rec->status = RPKT_S_L4_OTHER;
+    }
+}
+
+/* Load chain `first .. last-1` of the caller's segment list into `m`, clamping
+ * each segment to the arena exactly as the device does (include/rpkt_gpu.h). */
+static void chain_load(mchain_t* m, const uint8_t* buf, uint64_t buf_bytes, const uint32_t* segs,
+                       uint32_t first, uint32_t last) {
+    m->base = buf;
+    m->nb_segs = last - first;
+    m->pkt_len = 0;
+    for (uint32_t k = 0; k < m->nb_segs; k++) {
+        uint64_t o = segs[2 * (first + k)], l = segs[2 * (first + k) + 1];
+        if (o > buf_bytes) o = buf_bytes;
+        if (o + l > buf_bytes) l = buf_bytes - o;
+        m->off[k] = o;
+        m->len[k] = l;
+        m->pkt_len += l;
+    }
+}
+
+/* Batch driver with the arguments of rpkt_gpu_parse_chains: chain p is segments
+ * [a, b) with a = min(first[p], n_segs), b = min(max(first[p+1], a), n_segs). */
+void oracle_parse_chains(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* segs,
+                         uint32_t n_segs, const uint32_t* chain_first, uint32_t n_chains,
+                         uint32_t flags, uint32_t n_buckets, rpkt_rec_t* recs,
+                         uint64_t* flow_ev) {
+    uint32_t cap = 0;
+    uint64_t *off = NULL, *len = NULL;
+    for (uint32_t p = 0; p < n_chains; p++) {
+        uint32_t a = chain_first[p] < n_segs ? chain_first[p] : n_segs;
+        uint32_t b = chain_first[p + 1] > a ? chain_first[p + 1] : a;
+        if (b > n_segs) b = n_segs;
+        if (b - a > cap) {
+            cap = b - a;
+            off = realloc(off, cap * sizeof(uint64_t));
+            len = realloc(len, cap * sizeof(uint64_t));
+            if (!off || !len) die("out of memory");
+        }
+        mchain_t m = {buf, off, len, 0, 0};
+        chain_load(&m, buf, buf_bytes, segs, a, b);
+        parse_pbuf(&m, flags, &recs[p]);
+        if (flow_ev) flow_ev[p] = oracle_flow_event(&recs[p], n_buckets);
+    }
+    free(off);
+    free(len);
+}
+
+/* Replay a script of Pbuf operations over a chain of segment lengths (no data),
+ * for the assertions of rpkt-dpdk/tests/pbuf.rs.  ops[2i] = 0 new, 1 advance,
+ * 2 trim_off; ops[2i+1] = count.  After each op, out[6i..6i+5] = cursor,
+ * chunk().len(), remaining(), chunk_headroom(), num_segs(), pkt_len(). */
+void oracle_pbuf_script(const uint32_t* seg_lens, uint32_t n, const uint64_t* ops,
+                        uint32_t n_ops, uint64_t* out) {
+    uint64_t* off = calloc(n ? n : 1, sizeof(uint64_t));
+    uint64_t* len = calloc(n ? n : 1, sizeof(uint64_t));
+    mchain_t m = {NULL, off, len, 0, 0};
+    pbuf_t p;
+    for (uint32_t i = 0; i < n_ops; i++) {
+        if (ops[2 * i] == 0) {
+            m.nb_segs = n;
+            m.pkt_len = 0;
+            uint64_t o = 0;
+            for (uint32_t k = 0; k < n; k++) {
+                off[k] = o;
+                len[k] = seg_lens[k];
+                o += 4096;
+                m.pkt_len += seg_lens[k];
+            }
+            pbuf_new(&p, &m);
+        } else if (ops[2 * i] == 1) {
+            pbuf_advance(&p, ops[2 * i + 1]);
+        } else {
+            pbuf_trim_off(&p, ops[2 * i + 1]);
+        }
+        out[6 * i + 0] = pbuf_cursor(&p);
+        out[6 * i + 1] = p.chunk_len;
+        out[6 * i + 2] = pbuf_remaining(&p);
+        out[6 * i + 3] = pbuf_headroom(&p);
+        out[6 * i + 4] = m.nb_segs;
+        out[6 * i + 5] = m.pkt_len;
+    }
+    free(off);
+    free(len);
+}

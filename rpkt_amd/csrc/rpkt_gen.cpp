@@ -237,7 +237,14 @@ Spec spec_for(int config, uint64_t seed, uint32_t i, uint32_t len, Rng& r) {
             s.pad = r.chance(1000) ? (int)r.below(9) : 0;
             s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
             break;
-        default: {  // 6: fuzz — every status, odd alignments, tiny frames
+        case 7:  // jumbo frames (rpkt-dpdk/examples/jumboframe_tx.rs:45, PACKET_LEN 8000)
+            s.tcp = r.below(2) == 1; s.src = gen_ip(172, 74, 8192, r.below(8192));
+            s.sport = 1024 + r.below(4096); s.dport = s.tcp ? 80 : 161;
+            s.rand_payload = true;
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            s.ident = i & 0xffff;
+            break;
+        default: {  // 6 (and 8, chained): fuzz — every status, odd alignments, tiny frames
             s.nvlan = (int)r.below(4) == 0 ? (int)r.below(3) : 0;
             s.tpid0 = r.below(2) ? 0x88a8 : 0x8100;
             s.ihl = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
@@ -265,7 +272,7 @@ void fill_range(int config, uint64_t seed, uint64_t first, const uint32_t* offse
         uint32_t len = lens[i];
         uint64_t off = offsets ? offsets[i] : (uint64_t)i * stride;
         Spec s = spec_for(config, seed, (uint32_t)gi, len, r);
-        if (config == 6 && s.fault == 1) {
+        if ((config == 6 || config == 8) && s.fault == 1) {
             // truncation: build a full frame then cut it at a random length
             uint32_t full = len + 64;
             std::vector<uint8_t> tmp(full);
@@ -294,6 +301,12 @@ void rpkt_gen_lengths(int config, uint64_t seed, uint64_t first, uint32_t n, uin
             case 3: L = 1500; break;
             case 4: { uint32_t k = r.below(12); L = k < 7 ? 64 : (k < 11 ? 570 : 1500); break; }
             case 5: L = 64 + r.below(1518 - 64 + 1); break;
+            case 7: L = 8000; break;
+            case 8: {
+                uint32_t k = r.below(4);
+                L = k == 0 ? r.below(301) : (k == 1 ? 1000 + r.below(600) : 1600 + r.below(7401));
+                break;
+            }
             default: L = r.below(8) == 0 ? 1000 + r.below(600) : r.below(301); break;
         }
         lens[i] = L;
@@ -311,6 +324,24 @@ int rpkt_gen_fill(int config, uint64_t seed, uint64_t first, uint32_t n, const u
         uint32_t lo = (uint32_t)((uint64_t)n * t / threads);
         uint32_t hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
         th.emplace_back(fill_range, config, seed, first, offsets, lens, stride, lo, hi, frames);
+    }
+    for (auto& x : th) x.join();
+    return 0;
+}
+
+// Scatter packed frame bytes into mbuf-style segments: segment k copies lens[k]
+// bytes from src + src_off[k] to dst + dst_off[k] (the chain layouts of gen.py).
+int rpkt_gen_scatter(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
+                     const uint32_t* lens, uint32_t n_segs, uint8_t* dst, int threads) {
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n_segs / 1024 + 1) threads = (int)(n_segs / 1024 + 1);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        uint32_t lo = (uint32_t)((uint64_t)n_segs * t / threads);
+        uint32_t hi = (uint32_t)((uint64_t)n_segs * (t + 1) / threads);
+        th.emplace_back([=] {
+            for (uint32_t k = lo; k < hi; k++) memcpy(dst + dst_off[k], src + src_off[k], lens[k]);
+        });
     }
     for (auto& x : th) x.join();
     return 0;

@@ -54,6 +54,7 @@ struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit 
     uint32_t last[kWave];            // stream: scan value at a range's last chunk
 };
 static_assert(sizeof(WaveScratch) * kWavesPerBlock * 4 <= 160 * 1024, "4 blocks per CU");
+static_assert((64 * 21 + 705) * 4 <= 64 * 132, "chain scratch fits the window area");
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -700,6 +701,388 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     flush_records<V != 8>(W, lane, recs, p0, n);
 }
 
+// ---- mbuf chains: the same parse over rpkt-dpdk's Pbuf ----
+// A chain is a list of (offset, data_len) segments of one arena.  Over a Pbuf the
+// generic views test header sizes against chunk(), the rest of the segment that holds
+// the header's first byte (pbuf.rs:48-57, 86-96), and totals against remaining()
+// (pbuf.rs:98-101); trim_off cuts the packet end (pbuf.rs:117-140).  Segment 0 is
+// windowed into LDS like a frame, so every header that starts inside it is parsed by
+// the window path; a header that starts exactly at segment 0's end (the only way
+// past it) is read from global memory byte-wise on a rare path.  The L4 bytes past
+// the window are summed by the flattened chunk stream over (chain, segment) items,
+// each item's sum brought to segment 0's byte phase before it is added.
+struct ChainSrc {
+    const uint2* segs;
+    uint32_t fb;
+    __device__ __forceinline__ Frame seg(uint32_t k) const {
+        const uint2 v = segs[k];
+        const uint32_t off = v.x < fb ? v.x : fb;
+        const uint32_t len = v.y < fb - off ? v.y : fb - off;
+        return Frame{off, len};
+    }
+};
+
+__device__ __forceinline__ uint32_t gbyte(__amdgpu_buffer_rsrc_t rs, uint32_t a) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)a, 0, 0);
+}
+// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout)
+__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t (&F)[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        F[k] = gbyte(rs, a + 4 * k) | (gbyte(rs, a + 4 * k + 1) << 8) |
+               (gbyte(rs, a + 4 * k + 2) << 16) | (gbyte(rs, a + 4 * k + 3) << 24);
+}
+// checksum::from_slice over n bytes at absolute `a` (rpkt/src/checksum.rs:33-62)
+__device__ __forceinline__ uint32_t gsum_be(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t n) {
+    uint32_t acc = 0, k = 0;
+    for (; k + 1 < n; k += 2) acc += (gbyte(rs, a + k) << 8) | gbyte(rs, a + k + 1);
+    if (k < n) acc += gbyte(rs, a + k) << 8;
+    return fold16(acc);
+}
+
+// Chunk at logical cursor c > 0 of segments [a, b) under the packet end `limit`: the
+// rest of the first segment whose end passes c (empty segments skipped, as
+// advance_common walks), cut at limit.  `abs` = the chunk's first byte.
+__device__ __forceinline__ uint32_t chain_chunk(const ChainSrc& S, uint32_t a, uint32_t b,
+                                                uint32_t c, uint32_t limit, uint32_t& abs) {
+    uint32_t cum = 0;
+    for (uint32_t k = a; k < b; ++k) {
+        const Frame s = S.seg(k);
+        const uint32_t end = cum + s.len;
+        if (end > c) {
+            abs = s.off + (c - cum);
+            return (end < limit ? end : limit) - c;
+        }
+        cum = end;
+    }
+    abs = S.fb;
+    return 0;
+}
+
+// Lane-per-chain parse: parse_lane with the chunk/remaining distinction of a Pbuf.
+// C = segment 0's length: headers starting below C are read from the LDS window.
+__device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane, Frame s0,
+                                                 uint32_t pkt, const ChainSrc& S, uint32_t a,
+                                                 uint32_t b, __amdgpu_buffer_rsrc_t rs,
+                                                 uint32_t flags, LaneRec& L) {
+    const uint32_t ph = s0.off & 15u;
+    const uint8_t* slot = &W.win[lane * kSlot];
+    uint32_t* w = L.w;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    const uint32_t C = s0.len;                                 // Pbuf::new, pbuf.rs:19-34
+    L.stream_s = L.stream_e = L.l4_part = L.l4_start_abs = L.pseudo = 0;
+    L.want_l4 = false;
+    w[19] = pkt;
+    uint32_t status = RPKT_S_OK;
+
+    uint32_t E[6];
+    {
+        const uint32_t a0 = ph & ~3u, sh = ph & 3u;
+        uint32_t R[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) R[k] = lds32(slot, a0 + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) E[k] = align_bytes(R[k + 1], R[k], sh);
+    }
+    if (C < 14) {                                              // ether/generated.rs:36
+        L.status = RPKT_S_ETH_SHORT;
+        w[0] = RPKT_S_ETH_SHORT;
+        return;
+    }
+    w[1] = E[0];
+    w[2] = E[1];
+    w[3] = E[2];
+    const uint32_t eth_et = be16_lo(E[3]);
+    uint32_t nvlan = 0, et = eth_et, c = 14;
+#pragma unroll
+    for (int v = 0; v < RPKT_MAX_VLAN; ++v) {                  // vlan/generated.rs:32-61
+        if (!is_tag(et)) break;
+        uint32_t T = 0, ck = 0;
+        if (c < C) {
+            ck = C - c;
+            T = v == 0 ? align_bytes(E[4], E[3], 2) : align_bytes(E[5], E[4], 2);
+        } else if (c < pkt) {
+            uint32_t ab;
+            ck = chain_chunk(S, a, b, c, pkt, ab);
+            T = gbyte(rs, ab) | (gbyte(rs, ab + 1) << 8) | (gbyte(rs, ab + 2) << 16) |
+                (gbyte(rs, ab + 3) << 24);
+        }
+        if (ck < 4) {
+            status = RPKT_S_VLAN_SHORT;
+            break;
+        }
+        et = be16_hi(T);
+        w[4] |= be16_lo(T) << (16 * v);
+        w[5] |= et << (16 * v);
+        nvlan += 1;
+        c += 4;
+    }
+    w[0] = (nvlan << 8) | (eth_et << 16);
+    if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+
+    // Ipv4::parse (ipv4/generated.rs:35-51): chunk vs remaining
+    const uint32_t l3 = c;
+    w[16] = l3;
+    Hdr6 ip;
+    uint32_t ck3 = 0, ab3 = 0;
+    const bool fast3 = l3 < C;
+    if (fast3) {
+        ck3 = C - l3;
+        read_hdr(slot, ph + l3, ip);
+    } else {
+        if (l3 < pkt) ck3 = chain_chunk(S, a, b, l3, pkt, ab3);
+        gread20(rs, ck3 ? ab3 : S.fb, ip.F);
+    }
+    const uint32_t vhl = ip.F[0] & 0xffu;
+    const uint32_t ihl4 = (vhl & 0xfu) * 4u;
+    const uint32_t tot = be16_hi(ip.F[0]);
+    if (ck3 < 20) status = RPKT_S_IP_SHORT;
+    else if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
+    else if (ihl4 > ck3) status = RPKT_S_IP_IHL_GT_LEN;
+    else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
+    else if (tot > pkt - l3) status = RPKT_S_IP_TOT_GT_LEN;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+    const uint32_t proto = (ip.F[2] >> 8) & 0xffu;
+    const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
+    w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
+    w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
+    w[8] = (ip.F[2] & 0xffffu) | (be16_hi(ip.F[2]) << 16);
+    w[9] = src;
+    w[10] = dst;
+    if (flags & RPKT_F_IP_SUM)
+        w[18] = fast3 ? be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4),
+                               s0.off + l3)
+                      : gsum_be(rs, ab3, ihl4);
+    const uint32_t l4 = l3 + ihl4, limit = l3 + tot;           // Ipv4::payload :115-127
+    const uint32_t l4rem = tot - ihl4;
+    w[16] |= l4 << 16;
+    w[17] = l4 | (l4rem << 16);
+
+    // Udp::parse / Tcp::parse against the chunk at l4 under the trimmed end
+    Hdr6 h4;
+    uint32_t ck4 = 0, ab4 = 0;
+    const bool fast4 = l4 < C;
+    if (fast4) {
+        ck4 = (C < limit ? C : limit) - l4;
+        read_hdr(slot, ph + l4, h4);
+    } else {
+        if (l4 < limit) ck4 = chain_chunk(S, a, b, l4, limit, ab4);
+        gread20(rs, ck4 ? ab4 : S.fb, h4.F);
+    }
+    uint32_t l4len = 0;
+    if (proto == 17u) {
+        const uint32_t ulen = be16_lo(h4.F[1]);
+        if (ck4 < 8) status = RPKT_S_UDP_SHORT;
+        else if (ulen < 8 || ulen > l4rem) status = RPKT_S_UDP_BAD_LEN;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[14] = ulen;
+            w[15] = be16_hi(h4.F[1]);
+            w[17] = (l4 + 8) | ((ulen - 8) << 16);
+            l4len = ulen;
+        }
+    } else if (proto == 6u) {
+        const uint32_t hl = ((h4.F[3] >> 4) & 0xfu) * 4u;
+        if (ck4 < 20) status = RPKT_S_TCP_SHORT;
+        else if (hl < 20 || hl > ck4) status = RPKT_S_TCP_BAD_DOFF;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[12] = bswap32(h4.F[1]);
+            w[13] = bswap32(h4.F[2]);
+            w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
+            w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
+            w[17] = (l4 + hl) | ((l4rem - hl) << 16);
+            l4len = l4rem;
+        }
+    } else {
+        status = RPKT_S_L4_OTHER;
+    }
+    w[0] |= status;
+    L.status = status;
+    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+        L.want_l4 = true;
+        L.pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto + l4len;
+        const uint32_t e = l4 + l4len;
+        L.l4_start_abs = s0.off + l4;                          // segment 0's byte phase
+        if (fast4) {
+            const uint32_t win_end = kWin - ph;
+            uint32_t e_in = e < win_end ? e : win_end;
+            e_in = e_in < C ? e_in : C;
+            L.l4_part = raw_range_sum(slot, h4.R, h4.a0, ph + l4, ph + e_in);
+            L.stream_s = e_in;
+        } else {
+            L.stream_s = l4;
+        }
+        L.stream_e = e;                                        // logical, not absolute
+    }
+}
+
+// Sum of the logical range [ss, se) of this lane's chain, in segment 0's byte phase,
+// for every lane of the wave.  Items (chain, segment intersecting its range) are
+// flattened in chain order; each round streams 64 of them with wave_stream_sum.
+// An item's logical start is its owner's running cursor plus a segmented prefix sum
+// of the round's segment lengths.  Scratch: the window area past the staged records
+// (dwords [0, 513) of it; the caller keeps per-lane values at [513, 705)).
+__device__ __forceinline__ uint32_t chain_stream(WaveScratch& W, __amdgpu_buffer_rsrc_t rs,
+                                                 uint32_t fb, const ChainSrc& S, uint32_t a,
+                                                 uint32_t b, uint32_t off0, uint32_t ss,
+                                                 uint32_t se, int lane) {
+    uint32_t k = 0, fi = 0, ls0 = 0;
+    if (se > ss) {
+        uint32_t cum = 0;
+        for (uint32_t j = a; j < b; ++j) {
+            const uint32_t len = S.seg(j).len;
+            if (cum + len > ss && cum < se) {
+                if (k == 0) {
+                    fi = j;
+                    ls0 = cum;
+                }
+                ++k;
+            }
+            cum += len;
+            if (cum >= se) break;
+        }
+    }
+    const uint32_t incl = wave_incl_scan(k);
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    if (T == 0) return 0;                                      // wave-uniform
+    uint32_t* X = rec_stage(W) + kWave * 21;
+    uint32_t* cb = X;                  // [65] first item of each lane
+    uint32_t* cfi = X + 65;            // first segment index
+    uint32_t* ccum = X + 129;          // logical start of the lane's next item
+    uint32_t* css = X + 193;
+    uint32_t* cse = X + 257;
+    uint32_t* cacc = X + 321;
+    uint32_t* citem = X + 385;         // [128] per-item state held over the stream
+    cb[lane] = incl - k;
+    if (lane == 63) cb[64] = incl;
+    cfi[lane] = fi | (off0 << 31);     // segment 0's byte parity in bit 31
+    ccum[lane] = ls0;
+    css[lane] = ss;
+    cse[lane] = se;
+    cacc[lane] = 0;
+    wave_sync();
+    for (uint32_t r0 = 0; r0 < T; r0 += kWave) {
+        const uint32_t g = r0 + lane;
+        const bool v = g < T;
+        uint32_t q = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (cb[q + step] <= g) q += step;
+        const uint32_t bq = cb[q];
+        const uint32_t t = g - bq;
+        const uint32_t fq = cfi[q];
+        const Frame sg = v ? S.seg((fq & 0x7fffffffu) + t) : Frame{0, 0};
+        const uint32_t x = sg.len;
+        const uint32_t inc = wave_incl_scan(x);
+        const uint32_t j0 = (bq > r0 ? bq : r0) - r0;          // owner's first lane this round
+        const uint32_t base = (uint32_t)__shfl((int)(inc - x), (int)j0, kWave);
+        const uint32_t ls = ccum[q] + (inc - x) - base;
+        const uint32_t lo = ls > css[q] ? ls : css[q];
+        const uint32_t he = ls + x, hi = he < cse[q] ? he : cse[q];
+        uint32_t s_abs = 0, e_abs = 0;
+        if (v && hi > lo) {
+            s_abs = sg.off + (lo - ls);
+            e_abs = sg.off + (hi - ls);
+        }
+        const uint32_t swap = ((sg.off - ls) ^ (fq >> 31)) & 1u;
+        const uint32_t last = v && (lane == kWave - 1 || t + 1 == cb[q + 1] - bq);
+        citem[lane] = q | (swap << 8) | (last << 9) | ((uint32_t)v << 10);   // kept in LDS
+        citem[kWave + lane] = he;                                               // over the stream
+        const uint32_t part = wave_stream_sum<2>(rs, fb, s_abs, e_abs, W, lane);
+        const uint32_t it = citem[lane];
+        const uint32_t qq = it & 63u;
+        if (it & (1u << 10)) {
+            uint32_t c = fold16(part);
+            atomicAdd(&cacc[qq], (it & (1u << 8)) ? bswap16(c) : c);
+        }
+        if (it & (1u << 9)) ccum[qq] = citem[kWave + lane];
+        wave_sync();
+    }
+    return cacc[lane];
+}
+
+template <bool L4>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
+                         const uint2* __restrict__ segs, uint32_t n_segs,
+                         const uint32_t* __restrict__ chain_first, uint32_t n, uint32_t flags,
+                         rpkt_rec_t* __restrict__ recs, uint64_t* __restrict__ flow_ev,
+                         uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(buf, fb);
+    const ChainSrc S{segs, fb};
+
+    // chain bounds, segment 0 and pkt_len (sum of data_len, saturating)
+    uint32_t a = 0, b = 0;
+    if (valid) {
+        const uint32_t f0 = chain_first[i], f1 = chain_first[i + 1];
+        a = f0 < n_segs ? f0 : n_segs;
+        b = f1 > a ? f1 : a;
+        b = b < n_segs ? b : n_segs;
+    }
+    Frame s0{0, 0};
+    uint32_t pkt = 0;
+    for (uint32_t k = a; k < b; ++k) {
+        const Frame s = S.seg(k);
+        if (k == a) s0 = s;
+        pkt = pkt + s.len < pkt ? 0xffffffffu : pkt + s.len;
+    }
+
+    // 1. segment 0's header window -> LDS
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, s0, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    wave_sync();
+
+    // 2. lane-per-chain parse
+    LaneRec L;
+    parse_chain_lane(W, lane, s0, pkt, S, a, b, rs, flags, L);
+    stage_record(W, lane, L.w);
+
+    // 3. L4 bytes past the window, across segments (the in-window part and the
+    //    pseudo header wait in LDS, past chain_stream's scratch)
+    if (L4) {
+        uint32_t* keep = rec_stage(W) + kWave * 21 + 513;
+        keep[lane] = L.l4_part;
+        keep[kWave + lane] = L.want_l4 ? (L.pseudo | 0x80000000u) : 0u;
+        keep[2 * kWave + lane] = L.l4_start_abs;
+        const uint32_t acc = chain_stream(W, rs, fb, S, a, b, s0.off, L.stream_s, L.stream_e, lane);
+        const uint32_t ps = keep[kWave + lane];
+        if (ps) {
+            const uint32_t sum = be_sum(keep[lane] + acc, keep[2 * kWave + lane]);
+            rec_stage(W)[lane * 21 + 18] |= fold16((ps & 0x7fffffffu) + sum) << 16;
+        }
+    }
+
+    // 4. records (+ flow events)
+    if ((flags & RPKT_F_FLOW_EV) && valid) {
+        const uint64_t ev = flow_event(L, rec_stage(W) + lane * 21, n_buckets);
+        __builtin_nontemporal_store(ev, &flow_ev[i]);
+    }
+    flush_records<true>(W, lane, recs, p0, n);
+}
+
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
 // chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
 template <int U, bool NT>
@@ -1009,6 +1392,28 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+
+int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,
+                          rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!c || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (c->n_chains == 0) return RPKT_OK;
+    if (!c->chain_first_dev || (c->n_segs && (!c->buf_dev || !c->segs_dev))) return RPKT_E_INVAL;
+    if (c->buf_bytes > kMaxFrameBytes || c->n_segs >= 0x80000000u) return RPKT_E_TOO_LARGE;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)c->segs_dev & 7u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (c->n_chains + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_chains_kernel<true> : parse_chains_kernel<false>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, c->buf_dev,
+                  (uint32_t)c->buf_bytes, (const uint2*)c->segs_dev, c->n_segs,
+                  c->chain_first_dev, c->n_chains, flags, recs_dev, (uint64_t*)flow_ev_dev,
+                  n_buckets);
 }
 
 // Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse

@@ -29,10 +29,18 @@ class Batch(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class Chains(ctypes.Structure):
+    """rpkt_chains_t"""
+    _fields_ = [("buf_dev", ctypes.c_void_p), ("buf_bytes", ctypes.c_uint64),
+                ("segs_dev", ctypes.c_void_p), ("chain_first_dev", ctypes.c_void_p),
+                ("n_segs", ctypes.c_uint32), ("n_chains", ctypes.c_uint32)]
+
+
 EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
            "rpkt_gpu_last_hip_error", "rpkt_gpu_device_info", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
-           "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains"]
+           "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
+           "rpkt_gpu_parse_chains"]
 
 _lib = None
 
@@ -74,6 +82,10 @@ def lib():
                                                ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_checksum_chains.restype = ctypes.c_int
+        L.rpkt_gpu_parse_chains.argtypes = [ctypes.POINTER(Chains), ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_void_p]
+        L.rpkt_gpu_parse_chains.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -204,3 +216,42 @@ def checksum_chains(buf, segs, chain_first, out=None, stream=None):
                                         ws.data_ptr(), _stream_ptr(stream))
     _check(rc, "rpkt_gpu_checksum_chains")
     return out
+
+
+class DeviceChains:
+    """Mbuf chains resident in HBM: the segment arena, (offset, length) u32 pairs and
+    the n + 1 chain_first indices (rpkt_chains_t)."""
+
+    def __init__(self, buf, segs, chain_first, n):
+        self.buf, self.segs, self.chain_first, self.n = buf, segs, chain_first, n
+
+    @classmethod
+    def from_host(cls, hc, device="cuda"):
+        torch = _torch()
+        buf = torch.from_numpy(np.ascontiguousarray(hc.buf)).to(device)
+        segs = torch.from_numpy(np.ascontiguousarray(hc.segs).view(np.int32).reshape(-1)).to(device)
+        first = torch.from_numpy(np.ascontiguousarray(hc.chain_first).view(np.int32)).to(device)
+        return cls(buf, segs, first, hc.n)
+
+    @property
+    def frames(self):
+        return self.buf
+
+    def desc(self):
+        return Chains(self.buf.data_ptr(), self.buf.numel(), self.segs.data_ptr(),
+                      self.chain_first.data_ptr(), self.segs.numel() // 2, self.n)
+
+
+def parse_chains(chains, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):
+    """rpkt_gpu_parse_chains: returns the uint8 record tensor (n * 80 bytes)."""
+    torch = _torch()
+    if recs is None:
+        recs = alloc_records(chains.n, chains.buf.device)
+    if flags & F_FLOW_EV and flow_ev is None:
+        flow_ev = torch.empty(chains.n, dtype=torch.int64, device=chains.buf.device)
+    d = chains.desc()
+    rc = lib().rpkt_gpu_parse_chains(ctypes.byref(d), flags, recs.data_ptr(),
+                                     flow_ev.data_ptr() if flow_ev is not None else None,
+                                     n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_chains")
+    return (recs, flow_ev) if flags & F_FLOW_EV else recs

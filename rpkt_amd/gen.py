@@ -7,6 +7,11 @@ Config ids follow BASELINE.json `configs` (1-based like SURVEY.md §8d):
   4 8,388,608 IMIX 64/570/1500 at 7:4:1, 50/50 TCP/UDP, packed + u32 offsets
   5 4,194,304 x U[64,1518] B, 802.1Q or QinQ, IPv4 options, TCP options, packed
   6 fuzz: every parse status, frames of 0..300 B and 1000..1600 B, packed
+  7 262,144 x 8000 B jumbo Ether/IPv4/{TCP,UDP} as mbuf chains: 2048-B data room,
+    2176-B mempool slots (128-B headroom) in shuffled order (rpkt-dpdk
+    examples/jumboframe_tx.rs:45; mempool_alloc(.., 2048 + 128, ..) in tests/pbuf.rs)
+  8 chain fuzz: config-6 style frames up to 9000 B cut into 1..6 segments at random
+    and header-boundary positions (empty segments included), odd slot alignments
 """
 import ctypes
 import os
@@ -15,10 +20,16 @@ import numpy as np
 
 from .build import GEN_LIB, build_gen
 
-DEFAULT_N = {1: 1000, 2: 1 << 20, 3: 1 << 20, 4: 8 << 20, 5: 4 << 20, 6: 1 << 16}
-DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6}
+DEFAULT_N = {1: 1000, 2: 1 << 20, 3: 1 << 20, 4: 8 << 20, 5: 4 << 20, 6: 1 << 16,
+             7: 1 << 18, 8: 1 << 15}
+DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8}
 STRIDED = {1: 64, 2: 64, 3: 1500}
-FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3}   # config 2 = extract + IPv4 header sum
+CHAINED = (7, 8)
+FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3}   # config 2 = extract + IPv4 header sum
+MBUF_ROOM, MBUF_HEADROOM = 2048, 128                      # RTE_MBUF_DEFAULT_DATAROOM, headroom
+# header-boundary cut positions for the chain fuzz (Ether 14, tags 18/22, IPv4 +20..60, L4 +8/20)
+FUZZ_CUTS = (0, 1, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 26, 30, 33, 34, 35, 38,
+             42, 46, 54, 58, 62, 66, 74, 82, 94, 102, 118, 128, 142)
 
 _lib = None
 
@@ -34,6 +45,9 @@ def lib():
                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
         L.rpkt_gen_fill.restype = ctypes.c_int
+        L.rpkt_gen_scatter.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_void_p,
+                                                               ctypes.c_int]
+        L.rpkt_gen_scatter.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -84,3 +98,94 @@ def make_batch(config, n=None, seed=None, threads=None, packed=None, first=0):
     lib().rpkt_gen_fill(config, seed, first, n, lens.ctypes.data, offsets32.ctypes.data, 0,
                         frames.ctypes.data, threads)
     return HostBatch(config, n, seed, frames[:total], offsets32, 0, 0)
+
+
+class HostChains:
+    """Frames as mbuf chains in host memory: an arena `buf` holding every segment,
+    `segs` = (offset, length) u32 pairs, chain p = segments chain_first[p] ..
+    chain_first[p+1]-1 (the rpkt_chains_t layout of include/rpkt_gpu.h)."""
+
+    def __init__(self, config, n, seed, buf, segs, chain_first, pkt_lens):
+        self.config, self.n, self.seed = config, n, seed
+        self.buf, self.segs, self.chain_first = buf, segs, chain_first
+        self.pkt_lens = pkt_lens
+
+    @property
+    def n_segs(self):
+        return int(self.segs.shape[0])
+
+    def lens(self):
+        return self.pkt_lens.astype(np.int64)
+
+    def frame(self, p):
+        """Chain p's bytes, concatenated (host-side view for tests)."""
+        a, b = int(self.chain_first[p]), int(self.chain_first[p + 1])
+        return b"".join(self.buf[o:o + l].tobytes() for o, l in self.segs[a:b])
+
+
+def _mbuf_cuts(lens, room):
+    nseg = np.maximum((lens + room - 1) // room, 1)
+    seg_len = np.full(int(nseg.sum()), room, dtype=np.int64)
+    last = np.cumsum(nseg) - 1
+    seg_len[last] = lens - (nseg - 1) * room
+    return nseg, seg_len
+
+
+def _fuzz_cuts(lens, rng):
+    nsegs, seg_lens = [], []
+    for L in lens.tolist():
+        k = int(rng.integers(1, 7))
+        cuts = rng.integers(0, L + 1, size=k - 1).tolist()
+        if k > 1 and rng.integers(0, 2):
+            cuts[0] = min(FUZZ_CUTS[int(rng.integers(0, len(FUZZ_CUTS)))], L)
+        cuts = sorted(cuts)
+        edges = [0] + cuts + [L]
+        nsegs.append(k)
+        seg_lens.extend(edges[i + 1] - edges[i] for i in range(k))
+    return np.array(nsegs, dtype=np.int64), np.array(seg_lens, dtype=np.int64)
+
+
+def make_chains(config, n=None, seed=None, threads=None, layout=None):
+    """Generate frames of `config` and lay them out as mbuf chains.  layout "mbuf":
+    2048-B segments in 2176-B slots (128-B headroom), slots in a seeded shuffled
+    order; "fuzz": random cuts (see FUZZ_CUTS), odd slot offsets."""
+    n = DEFAULT_N[config] if n is None else n
+    seed = DEFAULT_SEED[config] if seed is None else seed
+    threads = threads or min(16, os.cpu_count() or 1)
+    layout = layout or ("mbuf" if config == 7 else "fuzz")
+    hb = make_batch(config, n, seed, threads, packed=True)
+    lens = hb.lens()
+    rng = np.random.default_rng(seed * 7919 + 17)
+    if layout == "mbuf":
+        nseg, seg_len = _mbuf_cuts(lens, MBUF_ROOM)
+        slot_bytes, pad = MBUF_ROOM + MBUF_HEADROOM, np.full(seg_len.size, MBUF_HEADROOM)
+    else:
+        nseg, seg_len = _fuzz_cuts(lens, rng)
+        slot_bytes, pad = 0, rng.integers(0, 64, size=seg_len.size)
+    n_segs = seg_len.size
+    chain_first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(nseg, out=chain_first[1:])
+    # source offset of each segment inside the packed frame buffer
+    frame_base = np.repeat(hb.offsets[:-1].astype(np.int64), nseg)
+    cum = np.cumsum(seg_len) - seg_len
+    within = cum - cum[np.repeat(chain_first[:-1], nseg)]
+    src_off = (frame_base + within).astype(np.uint64)
+    slot = rng.permutation(n_segs).astype(np.int64)
+    if slot_bytes:                                   # fixed mempool slots
+        dst_off = (slot * slot_bytes + pad).astype(np.uint64)
+        total = n_segs * slot_bytes
+    else:                                            # packed in shuffled order, odd gaps
+        room = seg_len + pad
+        start = np.zeros(n_segs, dtype=np.int64)
+        start[slot] = np.cumsum(room[slot]) - room[slot]
+        dst_off = (start + pad).astype(np.uint64)
+        total = int(room.sum()) + 64
+    if total >= (1 << 32) - 256:
+        raise ValueError("chain arena of %d bytes exceeds the 4 GiB descriptor range" % total)
+    buf = np.zeros(total, dtype=np.uint8)
+    sl32 = seg_len.astype(np.uint32)
+    lib().rpkt_gen_scatter(hb.frames.ctypes.data, src_off.ctypes.data, dst_off.ctypes.data,
+                           sl32.ctypes.data, n_segs, buf.ctypes.data, threads)
+    segs = np.stack([dst_off.astype(np.uint32), sl32], axis=1)
+    return HostChains(config, n, seed, buf, np.ascontiguousarray(segs),
+                      chain_first.astype(np.uint32), lens.astype(np.uint32))

@@ -18,14 +18,15 @@ def rows(path):
 
 
 def main(prof, cfg, out):
+    kname = "parse_chains_kernel" if cfg in (7, 8) else "parse_kernel"
     tr = [r for r in rows(os.path.join(prof, "trace_kernel_trace.csv"))
-          if r["Kernel_Name"].startswith("parse_kernel")]
+          if r["Kernel_Name"].startswith(kname)]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr][5:]  # skip warmup
     stats = rows(os.path.join(prof, "trace_kernel_stats.csv"))
 
     def pmc(name):
         v = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, name + "_counter_collection.csv"))
-             if r["Kernel_Name"].startswith("parse_kernel")][5:]
+             if r["Kernel_Name"].startswith(kname)][5:]
         return sum(v) / len(v)
 
     fetch_kib, write_kib = pmc("fetch"), pmc("write")
@@ -37,7 +38,7 @@ def main(prof, cfg, out):
     res = {
         "config": cfg,
         "engine_build": build,
-        "kernel": "parse_kernel",
+        "kernel": kname,
         "launches": len(durs),
         "avg_duration_us": sum(durs) / len(durs) / 1e3,
         "fetch_size_kib": fetch_kib,
