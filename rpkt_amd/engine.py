@@ -228,7 +228,10 @@ class DeviceChains:
     @classmethod
     def from_host(cls, hc, device="cuda"):
         torch = _torch()
-        buf = torch.from_numpy(np.ascontiguousarray(hc.buf)).to(device)
+        host = np.ascontiguousarray(hc.buf)
+        if not host.flags.writeable:                 # torch refuses read-only numpy memory
+            host = host.copy()
+        buf = torch.from_numpy(host).to(device)
         segs = torch.from_numpy(np.ascontiguousarray(hc.segs).view(np.int32).reshape(-1)).to(device)
         first = torch.from_numpy(np.ascontiguousarray(hc.chain_first).view(np.int32)).to(device)
         return cls(buf, segs, first, hc.n)
