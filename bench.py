@@ -311,6 +311,77 @@ def run_config(cfg, args, rank, world, cpu=False):
     return out
 
 
+FORBID_IPS = ["192.168.5.%d" % k for k in range(3, 11)]    # loopback_rx.rs:42-51
+
+
+def ip_u32(s):
+    a, b, c, d = (int(x) for x in s.split("."))
+    return (a << 24) | (b << 16) | (c << 8) | d
+
+
+def run_tx(cfg, mode, args, rank, world):
+    """TX side: rpkt_gpu_build_batch (headers + both checksums filled, the
+    rpkt_build.rs path) or rpkt_gpu_forward_batch (loopback_rx rewrite) over a
+    resident batch whose records come from rpkt_gpu_parse_batch.  Rotates over 4
+    batches at 64 B like config 2.  Algorithmic bytes per frame: build = 80 B record
+    read + the frame read once (checksums) + the fixed header bytes written;
+    forward = 80 B record read + the rewritten header bytes of forwarded frames + 1."""
+    torch.cuda.empty_cache()
+    n = args.frames or gen.DEFAULT_N[cfg]
+    R = 4 if cfg == 2 else 1
+    hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
+           for r in range(R)]
+    dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
+    recs = [engine.parse_batch(db, 3) for db in dbs]
+    outs = [torch.empty(hb.n, dtype=torch.uint8, device="cuda") for hb in hbs]
+    forbid = torch.tensor([ip_u32(x) for x in FORBID_IPS], dtype=torch.int64, device="cuda")
+    dmac, smac = bytes([0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]), bytes([0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6])
+    stream = torch.cuda.current_stream()
+
+    def one(k):
+        j = k % R
+        if mode == "build":
+            engine.build_batch(dbs[j], recs[j], 3, built=outs[j], stream=stream)
+        else:
+            engine.forward_batch(dbs[j], recs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
+
+    k, t_w = 0, time.perf_counter()
+    while k < args.warmup or time.perf_counter() - t_w < args.min_warmup_s:
+        one(k)
+        k += 1
+        if k % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.steps):
+        one(k)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    r = as_records(recs[0].cpu().numpy())
+    lens = hbs[0].lens()
+    fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
+    if mode == "build":
+        alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
+    else:
+        kept = outs[0].cpu().numpy().astype(bool)
+        alg = hbs[0].n * (REC_BYTES + 1) + int(kept.sum()) * 42
+    achieved = alg / (kern_ms / 1e3) / 1e9
+    return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
+            "ms_per_step": wall / args.steps * 1e3, "frames_per_rank": hbs[0].n,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "alg_bytes_per_launch": alg},
+            "what": ("build: Udp|Tcp/Ipv4/Ether prepend_header + setters, IPv4 + L4 checksum "
+                     "fill" if mode == "build" else
+                     "forward: loopback_rx firewall (8 forbidden sources), swap + ttl-1 + "
+                     "MACs + checksum update")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -323,6 +394,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tx", default="build2,build3,forward2",
+                    help="TX-side legs reported under 'extra' (build<cfg>, forward<cfg>)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--dist-backend", default="nccl",
@@ -344,6 +417,9 @@ def main():
     for c in [int(x) for x in args.also.split(",") if x.strip()]:
         if c != args.config:
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
+    for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
+        mode = "build" if leg.startswith("build") else "forward"
+        extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
 
     if rank == 0:
         fb = {2: 64, 3: 1500, 7: 8000}.get(args.config)

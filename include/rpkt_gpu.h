@@ -236,6 +236,47 @@ typedef struct rpkt_chains {
 int rpkt_gpu_parse_chains(const rpkt_chains_t* chains, uint32_t flags, rpkt_rec_t* recs_dev,
                           rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
 
+/* ---- TX side ---------------------------------------------------------------- */
+
+/* Build flags: fill a checksum the way the NIC TX offload requested by the
+ * reference computes it (rpkt-dpdk/examples/loopback_rx.rs:133): field zeroed, the
+ * complement of the RFC 1071 sum; a UDP result of 0 is sent as 0xffff.  Without the
+ * flag the checksum field is the record's (a set_checksum setter value). */
+#define RPKT_BUILD_IP_CSUM 1u
+#define RPKT_BUILD_L4_CSUM 2u
+
+/* Batched header build (benches/rpkt/rpkt_build.rs:9-28): for each frame i of
+ * `batch` (payload already in place), write the headers the record recs_dev[i] asks
+ * for, as Udp|Tcp::prepend_header + setters, Ipv4::prepend_header + setters,
+ * VlanFrame::prepend_header + setters (n_vlan tags), EtherFrame::prepend_header +
+ * setters would: l3 = 14 + 4 n_vlan, l4 = l3 + IHL*4, UDP (protocol 17, 8 B) or TCP
+ * (6, the 20 fixed bytes; doff from l4_word6) or no L4 header.  Length fields are
+ * set from the frame span (prepend_header's remaining()): IPv4 packet_len =
+ * len - l3, UDP length = len - l4.  Option bytes are left as the buffer holds them.
+ * A frame too short for its headers (where prepend_header asserts) is left
+ * untouched; built_dev[i] (optional, n bytes) = 1 if written, else 0.  Records use
+ * the rpkt_rec_t getter layout, so building from parse records reproduces frames. */
+int rpkt_gpu_build_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev, uint32_t flags,
+                         uint8_t* built_dev, void* stream);
+
+/* Firewall forward (rpkt-dpdk/examples/loopback_rx.rs:96-140) over a parsed batch:
+ * frame i is forwarded when its record (from rpkt_gpu_parse_batch with
+ * RPKT_F_IP_SUM | RPKT_F_L4_SUM) is an untagged IPv4/UDP frame that parsed OK with
+ * a valid IPv4 sum and a valid UDP sum (or UDP checksum 0), the RX offload verdicts
+ * of the reference, and its source address is not in forbid_dev (n_forbid u32
+ * addresses, sorted ascending).  A forwarded frame is rewritten in place: ports and
+ * addresses swapped, TTL - 1 (wrapping), dst/src MAC = dmac/smac, IPv4 and UDP
+ * checksums recomputed (the reference's TX offload).  keep_dev[i] = 1 if forwarded. */
+typedef struct rpkt_fwd {
+    uint8_t         dmac[6];
+    uint8_t         smac[6];
+    const uint32_t* forbid_dev;
+    uint32_t        n_forbid;
+    uint32_t        reserved;
+} rpkt_fwd_t;
+int rpkt_gpu_forward_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
+                           const rpkt_fwd_t* fwd, uint8_t* keep_dev, void* stream);
+
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,
                         uint16_t dst_port, uint8_t protocol);

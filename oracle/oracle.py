@@ -63,6 +63,15 @@ def lib():
         L.oracle_pbuf_script.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                          ctypes.c_uint32, ctypes.c_void_p]
         L.oracle_pbuf_script.restype = None
+        L.oracle_build_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_build_batch.restype = None
+        L.oracle_forward_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_forward_batch.restype = None
         _lib = L
     return _lib
 
@@ -141,6 +150,32 @@ def pbuf_script(seg_lens, ops):
     lib().oracle_pbuf_script(_ptr(sl), sl.size, _ptr(o), len(ops), _ptr(out))
     keys = ("cursor", "chunk_len", "remaining", "headroom", "num_segs", "pkt_len")
     return [dict(zip(keys, (int(x) for x in out[6 * i:6 * i + 6]))) for i in range(len(ops))]
+
+
+def build_batch(frames, n, recs, flags=3, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_build_batch on the CPU: returns (new frames buffer, built flags)."""
+    out = np.array(frames, dtype=np.uint8, copy=True)
+    recs = np.ascontiguousarray(recs)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    built = np.zeros(n, dtype=np.uint8)
+    lib().oracle_build_batch(_ptr(out), out.size, _ptr(offs), stride, frame_len, n, _ptr(recs),
+                             flags, _ptr(built))
+    return out, built
+
+
+def forward_batch(frames, n, recs, dmac, smac, forbid=(), offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_forward_batch on the CPU: returns (new frames buffer, keep flags)."""
+    out = np.array(frames, dtype=np.uint8, copy=True)
+    recs = np.ascontiguousarray(recs)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    fb = np.ascontiguousarray(np.sort(np.asarray(forbid, dtype=np.uint32)))
+    dm = np.frombuffer(bytes(dmac), dtype=np.uint8).copy()
+    sm = np.frombuffer(bytes(smac), dtype=np.uint8).copy()
+    keep = np.zeros(n, dtype=np.uint8)
+    lib().oracle_forward_batch(_ptr(out), out.size, _ptr(offs), stride, frame_len, n, _ptr(recs),
+                               _ptr(dm), _ptr(sm), _ptr(fb) if fb.size else None, fb.size,
+                               _ptr(keep))
+    return out, keep
 
 
 def flow_count(ev, n_buckets):

@@ -1083,6 +1083,285 @@ void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
     flush_records<true>(W, lane, recs, p0, n);
 }
 
+// ---- TX side: header build and the loopback_rx forward rewrite ----
+// Both compose the fixed header bytes of a frame from an rpkt_rec_t in the frame's
+// LDS slot (slot byte x <-> absolute (off & ~15) + x, as for the parse window) and
+// write them back with wave-cooperative 16-B chunk stores: a chunk wholly inside a
+// frame's written ranges is one dwordx4 store, a partial one (at most the first and
+// last of each range) is stored byte by byte, so no byte outside the frame's own
+// header ranges is ever written (neighbouring frames are rewritten concurrently).
+__device__ __forceinline__ void put_be16(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+__device__ __forceinline__ void put_be32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+
+// Fixed header bytes from record words (include/rpkt_gpu.h layout): Ethernet, n_vlan
+// tags, the 20 IPv4 bytes at l3, the UDP header or the 20 TCP bytes at l4.  These
+// are exactly the bytes prepend_header + setters write (ether/generated.rs:71-88,
+// vlan/generated.rs:73-100, ipv4/generated.rs:130-206, udp/generated.rs:79-104,
+// tcp/generated.rs:135-224); option bytes are not touched.
+__device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20], uint32_t nv,
+                                             uint32_t l3, uint32_t l4, uint32_t proto,
+                                             uint32_t ip_len, uint32_t udp_len, uint32_t ip_ck,
+                                             uint32_t l4_ck) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s[k] = (uint8_t)(w[1 + k / 4] >> (8 * (k % 4)));
+    put_be16(s + 12, w[0] >> 16);
+#pragma unroll
+    for (uint32_t v = 0; v < RPKT_MAX_VLAN; ++v) {
+        if (v < nv) {
+            put_be16(s + 14 + 4 * v, w[4] >> (16 * v));
+            put_be16(s + 16 + 4 * v, w[5] >> (16 * v));
+        }
+    }
+    uint8_t* ip = s + l3;
+    ip[0] = (uint8_t)w[6];
+    ip[1] = (uint8_t)(w[6] >> 8);
+    put_be16(ip + 2, ip_len);
+    put_be16(ip + 4, w[7]);
+    put_be16(ip + 6, w[7] >> 16);
+    ip[8] = (uint8_t)w[8];
+    ip[9] = (uint8_t)(w[8] >> 8);
+    put_be16(ip + 10, ip_ck);
+    put_be32(ip + 12, w[9]);
+    put_be32(ip + 16, w[10]);
+    uint8_t* t = s + l4;
+    if (proto == 17u) {
+        put_be16(t, w[11]);
+        put_be16(t + 2, w[11] >> 16);
+        put_be16(t + 4, udp_len);
+        put_be16(t + 6, l4_ck);
+    } else if (proto == 6u) {
+        put_be16(t, w[11]);
+        put_be16(t + 2, w[11] >> 16);
+        put_be32(t + 4, w[12]);
+        put_be32(t + 8, w[13]);
+        put_be16(t + 12, w[14]);
+        put_be16(t + 14, w[14] >> 16);
+        put_be16(t + 16, l4_ck);
+        put_be16(t + 18, w[15] >> 16);
+    }
+}
+
+// Absolute-phase word sum of LDS slot bytes [s, e) (any alignment).
+__device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t s, uint32_t e) {
+    uint32_t acc = 0;
+    for (uint32_t a = s & ~3u; a < e; a += 4)
+        acc += halves(lds32(slot, a) & byte_mask((int)s - (int)a, (int)e - (int)a));
+    return acc;
+}
+
+__device__ __forceinline__ void load_record(const rpkt_rec_t* recs, uint32_t i, uint32_t (&w)[20]) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(recs + i);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const u32x4 v = p[k];
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+}
+
+// Store frame bytes [r0, r1) and [r2, r3) (frame-relative, per owning lane) from the
+// tile's LDS slots.  Ranges lie inside the LDS window (< kWin - phase).
+__device__ __forceinline__ void write_back(uint8_t* frames, const WaveScratch& W, int lane,
+                                           uint32_t off, uint32_t r0, uint32_t r1, uint32_t r2,
+                                           uint32_t r3) {
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) {
+        const int c = k * kWave + lane;
+        const int q = c / kWinChunks, j = c % kWinChunks;
+        const uint32_t qo = (uint32_t)__shfl((int)off, q, kWave);
+        const uint32_t a0 = (uint32_t)__shfl((int)r0, q, kWave), a1 = (uint32_t)__shfl((int)r1, q, kWave);
+        const uint32_t a2 = (uint32_t)__shfl((int)r2, q, kWave), a3 = (uint32_t)__shfl((int)r3, q, kWave);
+        const uint32_t base = (qo & ~15u) + 16u * j;         // chunk's absolute address
+        // chunk-relative byte mask of the two ranges
+        uint32_t m = 0;
+        {
+            const int lo = (int)(qo + a0) - (int)base, hi = (int)(qo + a1) - (int)base;
+            const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
+            if (h > l) m |= ((1u << h) - 1u) & ~((1u << l) - 1u);
+        }
+        {
+            const int lo = (int)(qo + a2) - (int)base, hi = (int)(qo + a3) - (int)base;
+            const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
+            if (h > l) m |= ((1u << h) - 1u) & ~((1u << l) - 1u);
+        }
+        if (!m) continue;
+        const uint8_t* src = &W.win[q * kSlot + 16 * j];
+        if (m == 0xffffu) {
+            const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+            *reinterpret_cast<u32x4*>(frames + base) = u32x4{s4[0], s4[1], s4[2], s4[3]};
+        } else {
+            for (int b = 0; b < 16; ++b)
+                if (m & (1u << b)) frames[base + b] = src[b];
+        }
+    }
+}
+
+// rpkt_gpu_build_batch: window -> headers composed in LDS -> checksums (IPv4 over the
+// slot; L4 over the slot plus the payload stream past the window) -> write-back.
+template <bool L4FILL>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
+                  uint32_t stride, uint32_t frame_len, uint32_t n,
+                  const rpkt_rec_t* __restrict__ recs, uint32_t flags, uint8_t* __restrict__ built) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    if (valid) load_record(recs, i, w);
+    wave_sync();
+
+    const uint32_t ph = fr.off & 15u, len = fr.len;
+    uint8_t* slot = &W.win[lane * kSlot];
+    const uint32_t nv = (w[0] >> 8) & 0xffu;
+    const uint32_t l3 = 14u + 4u * nv;
+    const uint32_t ihl4 = (w[6] & 0xfu) * 4u;
+    const uint32_t l4 = l3 + ihl4;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;
+    const uint32_t doff4 = ((w[14] >> 12) & 0xfu) * 4u;
+    const uint32_t l4hdr = proto == 17u ? 8u : (proto == 6u ? doff4 : 0u);
+    const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
+    const bool ok = valid && nv <= RPKT_MAX_VLAN && ihl4 >= 20u && !(proto == 6u && doff4 < 20u) &&
+                    len >= l4 + l4hdr && len - l3 <= 65535u &&
+                    !(proto == 17u && len - l4 > 65535u);
+    const bool fill_ip = ok && (flags & RPKT_BUILD_IP_CSUM);
+    const bool fill_l4 = L4FILL && ok && fixed4;
+    if (ok)
+        emit_headers(slot + ph, w, nv, l3, l4, proto, len - l3, len - l4,
+                     fill_ip ? 0u : (w[8] >> 16), fill_l4 ? 0u : (w[15] & 0xffffu));
+    if (fill_ip) {
+        const uint32_t s = be_sum(lds_range_sum(slot, ph + l3, ph + l4), fr.off + l3);
+        put_be16(slot + ph + l3 + 10, ~s & 0xffffu);
+    }
+    if constexpr (L4FILL) {
+        // everything the checksum needs after the stream is packed into the slot's
+        // spare dword (bytes 128..131) and two registers, so the stream keeps its
+        // registers: pseudo header sum, in-window part, and
+        // info = fill | udp << 1 | l4 slot offset << 8
+        uint32_t part = 0, ss = 0, se = 0, pseudo = 0;
+        const uint32_t win_end = kWin - ph;
+        if (fill_l4) {
+            const uint32_t e_in = len < win_end ? len : win_end;
+            part = lds_range_sum(slot, ph + l4, ph + e_in);
+            if (len > e_in) {
+                ss = fr.off + e_in;
+                se = fr.off + len;
+            }
+            const uint32_t src = w[9], dst = w[10];
+            pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto +
+                     (len - l4);
+        }
+        *reinterpret_cast<uint32_t*>(slot + kWin) =
+            (uint32_t)fill_l4 | ((uint32_t)(proto == 17u) << 1) | ((ph + l4) << 8);
+        const uint32_t sp = wave_stream_sum<2>(rs, fb, ss, se, W, lane);
+        const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
+        if (info & 1u) {
+            const uint32_t at = info >> 8;                      // slot offset of the L4 header
+            const uint32_t sum = fold16(pseudo + be_sum(part + sp, (fr.off & ~15u) + at));
+            uint32_t ck = ~sum & 0xffffu;
+            const bool udp = info & 2u;
+            if (udp && ck == 0u) ck = 0xffffu;                  // RFC 768
+            put_be16(slot + at + (udp ? 6u : 16u), ck);
+        }
+    }
+    wave_sync();
+    write_back(frames, W, lane, fr.off, 0u, ok ? l4 + fixed4 : 0u, 0u, 0u);
+    if (built && valid) built[i] = ok ? 1 : 0;
+}
+
+// rpkt_gpu_forward_batch: record -> verdict -> rewritten fixed headers.  Checksums are
+// updated from the record's verify sums (RFC 1624): swapping addresses and ports
+// leaves every one's-complement sum unchanged, so only the TTL word and the zeroed
+// checksum field move the sum; both sums are of non-zero data, hence equal to a full
+// recompute bit for bit (tests compare with the oracle's full recompute).
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
+                    uint32_t stride, uint32_t frame_len, uint32_t n,
+                    const rpkt_rec_t* __restrict__ recs, rpkt_fwd_t fwd,
+                    uint8_t* __restrict__ keep) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    if (valid) load_record(recs, i, w);
+    const uint32_t l3 = w[16] & 0xffffu, l4 = w[16] >> 16;
+    const uint32_t ip_sum = w[18] & 0xffffu, l4_sum = w[18] >> 16;
+    const uint32_t udp_ck = w[15] & 0xffffu;
+    // untagged IPv4 (w0 = status | n_vlan << 8 | ethertype << 16), UDP, sums valid
+    bool fwd_ok = valid && (w[0] & 0xffffu) == RPKT_S_OK && (w[0] >> 16) == 0x0800u &&
+             ip_sum == 0xffffu && ((w[8] >> 8) & 0xffu) == 17u &&
+             (l4_sum == 0xffffu || udp_ck == 0u) && fr.len >= l4 + 8u;
+    if (fwd_ok && fwd.n_forbid) {                               // sorted: binary search
+        uint32_t lo = 0, hi = fwd.n_forbid;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (fwd.forbid_dev[mid] < w[9]) lo = mid + 1; else hi = mid;
+        }
+        if (lo < fwd.n_forbid && fwd.forbid_dev[lo] == w[9]) fwd_ok = false;
+    }
+    uint32_t r1 = 0, r2 = 0, r3 = 0;
+    if (fwd_ok) {
+        const uint32_t ttl = w[8] & 0xffu, proto = 17u;
+        const uint32_t old_w = (ttl << 8) | proto, new_w = (((ttl - 1u) & 0xffu) << 8) | proto;
+        const uint32_t ip_ck = ~fold16(ip_sum + (~(w[8] >> 16) & 0xffffu) + (~old_w & 0xffffu) +
+                                       new_w) & 0xffffu;
+        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu)) & 0xffffu;
+        if (u_ck == 0u) u_ck = 0xffffu;
+        uint32_t m[20];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) m[k] = w[k];
+        m[1] = fwd.dmac[0] | (fwd.dmac[1] << 8) | (fwd.dmac[2] << 16) | (fwd.dmac[3] << 24);
+        m[2] = fwd.dmac[4] | (fwd.dmac[5] << 8) | (fwd.smac[0] << 16) | (fwd.smac[1] << 24);
+        m[3] = fwd.smac[2] | (fwd.smac[3] << 8) | (fwd.smac[4] << 16) | (fwd.smac[5] << 24);
+        m[8] = (w[8] & ~0xffu) | ((ttl - 1u) & 0xffu);       // ttl - 1, wrapping
+        m[9] = w[10];
+        m[10] = w[9];
+        m[11] = (w[11] >> 16) | (w[11] << 16);
+        emit_headers(&W.win[lane * kSlot] + (fr.off & 15u), m, 0u, l3, l4, proto, w[6] >> 16,
+                     w[14] & 0xffffu, ip_ck, u_ck);
+        r1 = l3 + 20u;
+        r2 = l4;
+        r3 = l4 + 8u;
+    }
+    wave_sync();
+    write_back(frames, W, lane, fr.off, 0u, r1, r2, r3);
+    if (valid) keep[i] = fwd_ok ? 1 : 0;
+}
+
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
 // chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
 template <int U, bool NT>
@@ -1414,6 +1693,42 @@ int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* re
                   (uint32_t)c->buf_bytes, (const uint2*)c->segs_dev, c->n_segs,
                   c->chain_first_dev, c->n_chains, flags, recs_dev, (uint64_t*)flow_ev_dev,
                   n_buckets);
+}
+
+int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint32_t flags,
+                         uint8_t* built_dev, void* stream) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_BUILD_IP_CSUM | RPKT_BUILD_L4_CSUM)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)b->frames_dev & 15u) != 0)
+        return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true> : build_kernel<false>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
+                  b->stride, flen, b->n, recs_dev, flags, built_dev);
+}
+
+int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
+                           const rpkt_fwd_t* fwd, uint8_t* keep_dev, void* stream) {
+    if (!b || !recs_dev || !fwd || !keep_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev || (fwd->n_forbid && !fwd->forbid_dev)) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)b->frames_dev & 15u) != 0)
+        return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(forward_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
+                  b->stride, flen, b->n, recs_dev, *fwd, keep_dev);
 }
 
 // Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse

@@ -36,11 +36,18 @@ class Chains(ctypes.Structure):
                 ("n_segs", ctypes.c_uint32), ("n_chains", ctypes.c_uint32)]
 
 
+class Fwd(ctypes.Structure):
+    """rpkt_fwd_t"""
+    _fields_ = [("dmac", ctypes.c_uint8 * 6), ("smac", ctypes.c_uint8 * 6),
+                ("forbid_dev", ctypes.c_void_p), ("n_forbid", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
 EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
            "rpkt_gpu_last_hip_error", "rpkt_gpu_device_info", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
-           "rpkt_gpu_parse_chains"]
+           "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch"]
 
 _lib = None
 
@@ -86,6 +93,12 @@ def lib():
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                             ctypes.c_void_p]
         L.rpkt_gpu_parse_chains.restype = ctypes.c_int
+        L.rpkt_gpu_build_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_build_batch.restype = ctypes.c_int
+        L.rpkt_gpu_forward_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                             ctypes.POINTER(Fwd), ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_forward_batch.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -258,3 +271,36 @@ def parse_chains(chains, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=N
                                      n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_chains")
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
+
+
+def build_batch(batch, recs, flags=3, built=None, stream=None):
+    """rpkt_gpu_build_batch: write each frame's headers from its record, in place in
+    batch.frames (payload already there).  Returns the per-frame built flags (u8)."""
+    torch = _torch()
+    if built is None:
+        built = torch.empty(batch.n, dtype=torch.uint8, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_build_batch(ctypes.byref(d), recs.data_ptr(), flags, built.data_ptr(),
+                                    _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_build_batch")
+    return built
+
+
+def forward_batch(batch, recs, dmac, smac, forbid=None, keep=None, stream=None):
+    """rpkt_gpu_forward_batch (loopback_rx firewall rewrite) over a parsed batch.
+    forbid: int64 tensor of IPv4 addresses (host-order u32 values) on the device."""
+    torch = _torch()
+    if keep is None:
+        keep = torch.empty(batch.n, dtype=torch.uint8, device=batch.frames.device)
+    f = Fwd()
+    f.dmac[:] = list(bytes(dmac))
+    f.smac[:] = list(bytes(smac))
+    if forbid is not None and forbid.numel():
+        u32 = torch.sort(forbid.to(torch.int64) & 0xFFFFFFFF).values      # u32 order
+        forbid = u32.to(torch.int32)                                         # same bits
+        f.forbid_dev, f.n_forbid = forbid.data_ptr(), forbid.numel()
+    d = batch.desc()
+    rc = lib().rpkt_gpu_forward_batch(ctypes.byref(d), recs.data_ptr(), ctypes.byref(f),
+                                      keep.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_forward_batch")
+    return keep
