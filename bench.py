@@ -325,7 +325,8 @@ def run_tx(cfg, mode, args, rank, world):
     resident batch whose records come from rpkt_gpu_parse_batch.  Rotates over 4
     batches at 64 B like config 2.  Algorithmic bytes per frame: build = 80 B record
     read + the frame read once (checksums) + the fixed header bytes written;
-    forward = 80 B record read + the rewritten header bytes of forwarded frames + 1."""
+    forward (fused parse + verdict + rewrite) = the frame read once + the 42 rewritten
+    header bytes of forwarded frames + 1 B verdict."""
     torch.cuda.empty_cache()
     n = args.frames or gen.DEFAULT_N[cfg]
     R = 4 if cfg == 2 else 1
@@ -333,7 +334,8 @@ def run_tx(cfg, mode, args, rank, world):
            for r in range(R)]
     dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
     recs = [engine.parse_batch(db, 3) for db in dbs]
-    outs = [torch.empty(hb.n, dtype=torch.uint8, device="cuda") for hb in hbs]
+    outs = [torch.empty(hb.n * (64 if mode == "opts" else 1), dtype=torch.uint8, device="cuda")
+            for hb in hbs]
     forbid = torch.tensor([ip_u32(x) for x in FORBID_IPS], dtype=torch.int64, device="cuda")
     dmac, smac = bytes([0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]), bytes([0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6])
     stream = torch.cuda.current_stream()
@@ -342,8 +344,10 @@ def run_tx(cfg, mode, args, rank, world):
         j = k % R
         if mode == "build":
             engine.build_batch(dbs[j], recs[j], 3, built=outs[j], stream=stream)
+        elif mode == "opts":
+            engine.options_batch(dbs[j], recs[j], opts=outs[j], stream=stream)
         else:
-            engine.forward_batch(dbs[j], recs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
+            engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
 
     k, t_w = 0, time.perf_counter()
     while k < args.warmup or time.perf_counter() - t_w < args.min_warmup_s:
@@ -367,9 +371,15 @@ def run_tx(cfg, mode, args, rank, world):
     fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
     if mode == "build":
         alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
+    elif mode == "opts":                       # records + option slices read, 64 B written
+        ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
+        tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
+        slices = np.where(ip_parsed, r["l4_off"].astype(np.int64) - r["l3_off"] - 20, 0) + \
+            np.where(tcp, r["payload_off"].astype(np.int64) - r["l4_off"] - 20, 0)
+        alg = hbs[0].n * (REC_BYTES + 64) + int(slices.sum())
     else:
         kept = outs[0].cpu().numpy().astype(bool)
-        alg = hbs[0].n * (REC_BYTES + 1) + int(kept.sum()) * 42
+        alg = int(lens.sum()) + hbs[0].n + int(kept.sum()) * 42
     achieved = alg / (kern_ms / 1e3) / 1e9
     return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
             "ms_per_step": wall / args.steps * 1e3, "frames_per_rank": hbs[0].n,
@@ -378,8 +388,10 @@ def run_tx(cfg, mode, args, rank, world):
                          "alg_bytes_per_launch": alg},
             "what": ("build: Udp|Tcp/Ipv4/Ether prepend_header + setters, IPv4 + L4 checksum "
                      "fill" if mode == "build" else
-                     "forward: loopback_rx firewall (8 forbidden sources), swap + ttl-1 + "
-                     "MACs + checksum update")}
+                     "options: Ipv4OptionsIter + TcpOptionsIter walks of a parsed batch"
+                     if mode == "opts" else
+                     "forward: loopback_rx firewall fused (parse + both sums, 8 forbidden "
+                     "sources, swap + ttl-1 + MACs + checksum update)")}
 
 
 def main():
@@ -394,8 +406,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tx", default="build2,build3,forward2",
-                    help="TX-side legs reported under 'extra' (build<cfg>, forward<cfg>)")
+    ap.add_argument("--tx", default="build2,build3,forward2,opts5",
+                    help="legs beyond the parse reported under 'extra' (build<cfg>, "
+                         "forward<cfg>, opts<cfg>)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--dist-backend", default="nccl",
@@ -418,7 +431,7 @@ def main():
         if c != args.config:
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
     for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
-        mode = "build" if leg.startswith("build") else "forward"
+        mode = next(m for m in ("build", "forward", "opts") if leg.startswith(m))
         extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
 
     if rank == 0:

@@ -255,18 +255,20 @@ int rpkt_gpu_parse_chains(const rpkt_chains_t* chains, uint32_t flags, rpkt_rec_
  * len - l3, UDP length = len - l4.  Option bytes are left as the buffer holds them.
  * A frame too short for its headers (where prepend_header asserts) is left
  * untouched; built_dev[i] (optional, n bytes) = 1 if written, else 0.  Records use
- * the rpkt_rec_t getter layout, so building from parse records reproduces frames. */
+ * the rpkt_rec_t getter layout, so building from parse records reproduces frames.
+ * frames_dev and recs_dev 16-byte aligned. */
 int rpkt_gpu_build_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev, uint32_t flags,
                          uint8_t* built_dev, void* stream);
 
-/* Firewall forward (rpkt-dpdk/examples/loopback_rx.rs:96-140) over a parsed batch:
- * frame i is forwarded when its record (from rpkt_gpu_parse_batch with
- * RPKT_F_IP_SUM | RPKT_F_L4_SUM) is an untagged IPv4/UDP frame that parsed OK with
- * a valid IPv4 sum and a valid UDP sum (or UDP checksum 0), the RX offload verdicts
- * of the reference, and its source address is not in forbid_dev (n_forbid u32
+/* Firewall forward (rpkt-dpdk/examples/loopback_rx.rs:96-140), one fused pass per
+ * frame: the parse chain of rpkt_gpu_parse_batch with both sums, then frame i is
+ * forwarded when it is an untagged IPv4/UDP frame that parsed OK with a valid IPv4
+ * sum and a valid UDP sum (or UDP checksum 0) -- the RX offload verdicts of the
+ * reference -- and its source address is not in forbid_dev (n_forbid u32
  * addresses, sorted ascending).  A forwarded frame is rewritten in place: ports and
  * addresses swapped, TTL - 1 (wrapping), dst/src MAC = dmac/smac, IPv4 and UDP
- * checksums recomputed (the reference's TX offload).  keep_dev[i] = 1 if forwarded. */
+ * checksums recomputed (the reference's TX offload).  keep_dev[i] = 1 if forwarded;
+ * other frames are not written.  frames_dev 16-byte aligned. */
 typedef struct rpkt_fwd {
     uint8_t         dmac[6];
     uint8_t         smac[6];
@@ -274,8 +276,66 @@ typedef struct rpkt_fwd {
     uint32_t        n_forbid;
     uint32_t        reserved;
 } rpkt_fwd_t;
-int rpkt_gpu_forward_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
-                           const rpkt_fwd_t* fwd, uint8_t* keep_dev, void* stream);
+int rpkt_gpu_forward_batch(const rpkt_batch_t* batch, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
+                           void* stream);
+
+/* ---- Option iterators ----------------------------------------------------------- */
+
+/* Why an option walk stopped (the iterator's next() returned None). */
+enum rpkt_opt_stop {
+    RPKT_OPT_NONE = 0,       /* no option slice: that header was not parsed */
+    RPKT_OPT_END = 1,        /* the slice was consumed (buf.len() < 1) */
+    RPKT_OPT_UNKNOWN = 2,    /* a type outside the option group */
+    RPKT_OPT_MALFORMED = 3   /* the type's parse returned Err (short or bad length) */
+};
+
+/* Option kind indices (bits of *_kinds, 4-bit codes index + 1 in *_trace).
+ * TCP (tcp/generated.rs:1357-1366): 0 Eol, 1 Nop, 2 Mss, 3 WindowScale,
+ *   4 SackPermitted, 5 Sack, 6 Timestamp, 7 FastOpen.
+ * IPv4 (ipv4/generated.rs:1595-1604): 0 Eol, 1 Nop, 2 Timestamp (68),
+ *   3 RecordRoute (7), 4 RouteAlert (148), 5 CommercialSecurity (134),
+ *   6 StrictSourceRoute (137), 7 LooseSourceRoute (131). */
+
+/* One frame's option walks, 64 bytes: TcpOptionsIter over tcp.var_header_slice()
+ * and Ipv4OptionsIter over ipv4.var_header_slice(), with the getters of the options
+ * they yield (the last one of each kind). */
+typedef struct rpkt_opts {
+    uint8_t  tcp_count;         /*  0 options yielded                         */
+    uint8_t  tcp_stop;          /*  1 rpkt_opt_stop                           */
+    uint8_t  tcp_wscale;        /*  2 WindowScale::shift_count                */
+    uint8_t  tcp_sack_blocks;   /*  3 (Sack::header_len - 2) / 8              */
+    uint16_t tcp_kinds;         /*  4 bit k: kind index k yielded             */
+    uint16_t tcp_mss;           /*  6 Mss::mss                                */
+    uint32_t tcp_ts;            /*  8 Timestamp::ts                           */
+    uint32_t tcp_ts_echo;       /* 12 Timestamp::ts_echo                      */
+    uint32_t tcp_sack_left;     /* 16 first SACK block (Sack var_header_slice) */
+    uint32_t tcp_sack_right;    /* 20                                         */
+    uint16_t tcp_fo_len;        /* 24 FastOpen::header_len                    */
+    uint8_t  tcp_end;           /* 26 slice bytes consumed when the walk stopped */
+    uint8_t  ip_end;            /* 27                                         */
+    uint8_t  ip_count;          /* 28                                         */
+    uint8_t  ip_stop;           /* 29                                         */
+    uint16_t ip_kinds;          /* 30                                         */
+    uint16_t ip_route_alert;    /* 32 RouteAlert::data                        */
+    uint8_t  ip_rr_len;         /* 34 RecordRoute::header_len                 */
+    uint8_t  ip_rr_pointer;     /* 35 RecordRoute::pointer                    */
+    uint8_t  ip_ts_len;         /* 36 Timestamp::header_len                   */
+    uint8_t  ip_ts_pointer;     /* 37 Timestamp::pointer                      */
+    uint8_t  ip_ts_oflw_flg;    /* 38 oflw << 4 | flg                         */
+    uint8_t  ip_sr_pointer;     /* 39 Strict/LooseSourceRoute::pointer        */
+    uint32_t ip_sr_dest;        /* 40 Strict/LooseSourceRoute::dest_addr      */
+    uint32_t ip_cs_doi;         /* 44 CommercialSecurity::doi                 */
+    uint64_t tcp_trace;         /* 48 kinds of the first 16 options, 4 bits each (index + 1) */
+    uint64_t ip_trace;          /* 56                                         */
+} rpkt_opts_t;
+
+#define RPKT_OPTS_BYTES 64u
+
+/* Walk the IPv4 and TCP options of every frame of a parsed batch: recs_dev from
+ * rpkt_gpu_parse_batch on the same batch locates the slices (ip: [l3 + 20, l4),
+ * tcp: [l4 + 20, payload_off) for status OK / TCP).  opts_dev n * 64 B, 16-B aligned. */
+int rpkt_gpu_options_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
+                           rpkt_opts_t* opts_dev, void* stream);
 
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,

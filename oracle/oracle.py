@@ -72,6 +72,10 @@ def lib():
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         L.oracle_forward_batch.restype = None
+        L.oracle_options_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_options_batch.restype = None
         _lib = L
     return _lib
 
@@ -176,6 +180,18 @@ def forward_batch(frames, n, recs, dmac, smac, forbid=(), offsets=None, stride=0
                                _ptr(dm), _ptr(sm), _ptr(fb) if fb.size else None, fb.size,
                                _ptr(keep))
     return out, keep
+
+
+def options_batch(frames, n, recs, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_options_batch on the CPU: rpkt_opts_t per frame."""
+    from rpkt_amd.records import OPTS_DTYPE
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    recs = np.ascontiguousarray(recs)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    out = np.zeros(n, dtype=OPTS_DTYPE)
+    lib().oracle_options_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
+                               _ptr(recs), _ptr(out))
+    return out
 
 
 def flow_count(ev, n_buckets):

@@ -1,0 +1,129 @@
+/*
+ * rpkt_oracle_opts.c — CPU restatement of rpkt's option iterators, TEST
+ * INFRASTRUCTURE ONLY (tests/ and bench.py's cpu_baseline leg).
+ *
+ * TcpOptionsIter::next (rpkt/src/tcp/generated.rs:1387-1484) and Ipv4OptionsIter::next
+ * (rpkt/src/ipv4/generated.rs:1625-1722): dispatch on the first byte; the option's own
+ * parse decides (Some, advance by its header_len) or Err (None); an unknown type is
+ * None; an empty slice is None.  Per-type parse rules restated from the generated
+ * views (fixed length: chunk >= L and header_len == L; variable: chunk >= L and
+ * L <= header_len <= chunk):
+ *   TCP  Eol/Nop 1 B; Mss (2) ==4 :522-533; WindowScale (3) ==3 :664-675;
+ *        SackPermitted (4) ==2; Sack (5) var >=2 :942-953; Timestamp (8) ==10
+ *        :1086-1097; FastOpen (34) var >=2 :1236-1247.
+ *   IPv4 Eol/Nop 1 B; Timestamp (68) var >=4; RecordRoute (7) var >=3;
+ *        CommercialSecurity (134) var >=6; RouteAlert (148) ==4;
+ *        Loose/StrictSourceRoute (131/137) ==7.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/rpkt_gpu.h"
+
+static uint16_t be16(const uint8_t* p) { return (uint16_t)(((uint16_t)p[0] << 8) | p[1]); }
+static uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* returns the option length consumed (>0), 0 = malformed, -1 = unknown type;
+ * *kind = kind index */
+static int tcp_opt(const uint8_t* b, uint32_t n, int* kind) {
+    uint32_t t = b[0], hl = n >= 2 ? b[1] : 0;
+    switch (t) {
+        case 0: *kind = 0; return 1;
+        case 1: *kind = 1; return 1;
+        case 2: *kind = 2; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 3: *kind = 3; return (n >= 3 && hl == 3) ? 3 : 0;
+        case 4: *kind = 4; return (n >= 2 && hl == 2) ? 2 : 0;
+        case 5: *kind = 5; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        case 8: *kind = 6; return (n >= 10 && hl == 10) ? 10 : 0;
+        case 34: *kind = 7; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        default: return -1;
+    }
+}
+
+static int ip_opt(const uint8_t* b, uint32_t n, int* kind) {
+    uint32_t t = b[0], hl = n >= 2 ? b[1] : 0;
+    switch (t) {
+        case 0: *kind = 0; return 1;
+        case 1: *kind = 1; return 1;
+        case 68: *kind = 2; return (n >= 4 && hl >= 4 && hl <= n) ? (int)hl : 0;
+        case 7: *kind = 3; return (n >= 3 && hl >= 3 && hl <= n) ? (int)hl : 0;
+        case 148: *kind = 4; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 134: *kind = 5; return (n >= 6 && hl >= 6 && hl <= n) ? (int)hl : 0;
+        case 137: *kind = 6; return (n >= 7 && hl == 7) ? 7 : 0;
+        case 131: *kind = 7; return (n >= 7 && hl == 7) ? 7 : 0;
+        default: return -1;
+    }
+}
+
+void oracle_options_one(const uint8_t* f, uint32_t len, const rpkt_rec_t* r, rpkt_opts_t* o) {
+    memset(o, 0, sizeof(*o));
+    (void)len;
+    int ip_parsed = r->status == RPKT_S_OK || r->status >= RPKT_S_L4_OTHER;
+    if (ip_parsed) {
+        const uint8_t* b = f + r->l3_off + 20;            /* var_header_slice :41-44 */
+        uint32_t n = (uint32_t)(r->l4_off - r->l3_off - 20), pos = 0;
+        o->ip_stop = RPKT_OPT_END;
+        while (pos < n) {
+            int kind = 0, used = ip_opt(b + pos, n - pos, &kind);
+            if (used < 0) { o->ip_stop = RPKT_OPT_UNKNOWN; break; }
+            if (used == 0) { o->ip_stop = RPKT_OPT_MALFORMED; break; }
+            const uint8_t* p = b + pos;
+            if (kind == 2) { o->ip_ts_len = p[1]; o->ip_ts_pointer = p[2]; o->ip_ts_oflw_flg = p[3]; }
+            if (kind == 3) { o->ip_rr_len = p[1]; o->ip_rr_pointer = p[2]; }
+            if (kind == 4) o->ip_route_alert = be16(p + 2);
+            if (kind == 5) o->ip_cs_doi = be32(p + 2);
+            if (kind == 6 || kind == 7) { o->ip_sr_pointer = p[2]; o->ip_sr_dest = be32(p + 3); }
+            o->ip_kinds |= (uint16_t)(1u << kind);
+            if (o->ip_count < 16) o->ip_trace |= (uint64_t)(kind + 1) << (4 * o->ip_count);
+            o->ip_count++;
+            pos += (uint32_t)used;
+        }
+        o->ip_end = (uint8_t)pos;
+    }
+    if (r->status == RPKT_S_OK && r->ip_protocol == 6) {
+        uint32_t doff4 = (uint32_t)(r->l4_word6 >> 12) * 4;
+        const uint8_t* b = f + r->l4_off + 20;
+        uint32_t n = doff4 - 20, pos = 0;
+        o->tcp_stop = RPKT_OPT_END;
+        while (pos < n) {
+            int kind = 0, used = tcp_opt(b + pos, n - pos, &kind);
+            if (used < 0) { o->tcp_stop = RPKT_OPT_UNKNOWN; break; }
+            if (used == 0) { o->tcp_stop = RPKT_OPT_MALFORMED; break; }
+            const uint8_t* p = b + pos;
+            if (kind == 2) o->tcp_mss = be16(p + 2);
+            if (kind == 3) o->tcp_wscale = p[2];
+            if (kind == 5) {
+                o->tcp_sack_blocks = (uint8_t)((p[1] - 2) / 8);
+                o->tcp_sack_left = p[1] >= 6 ? be32(p + 2) : 0;
+                o->tcp_sack_right = p[1] >= 10 ? be32(p + 6) : 0;
+            }
+            if (kind == 6) { o->tcp_ts = be32(p + 2); o->tcp_ts_echo = be32(p + 6); }
+            if (kind == 7) o->tcp_fo_len = p[1];
+            o->tcp_kinds |= (uint16_t)(1u << kind);
+            if (o->tcp_count < 16) o->tcp_trace |= (uint64_t)(kind + 1) << (4 * o->tcp_count);
+            o->tcp_count++;
+            pos += (uint32_t)used;
+        }
+        o->tcp_end = (uint8_t)pos;
+    }
+}
+
+void oracle_options_batch(const uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
+                          uint32_t stride, uint32_t frame_len, uint32_t n, const rpkt_rec_t* recs,
+                          rpkt_opts_t* opts) {
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t off, len;
+        if (offsets) {
+            off = offsets[i];
+            len = offsets[i + 1] >= offsets[i] ? offsets[i + 1] - offsets[i] : 0;
+        } else {
+            off = (uint64_t)i * stride;
+            len = frame_len ? frame_len : stride;
+        }
+        if (off > frames_bytes) off = frames_bytes;
+        if (off + len > frames_bytes) len = frames_bytes - off;
+        oracle_options_one(frames + off, (uint32_t)len, &recs[i], &opts[i]);
+    }
+}

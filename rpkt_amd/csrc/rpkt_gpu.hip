@@ -1157,53 +1157,106 @@ __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t 
     return acc;
 }
 
-__device__ __forceinline__ void load_record(const rpkt_rec_t* recs, uint32_t i, uint32_t (&w)[20]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(recs + i);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const u32x4 v = p[k];
-        w[4 * k] = v.x;
-        w[4 * k + 1] = v.y;
-        w[4 * k + 2] = v.z;
-        w[4 * k + 3] = v.w;
-    }
+// Store frame bytes [r0, r1) and [r2, r3) (frame-relative, per owning lane) from the
+// tile's LDS slots.  Ranges lie inside the LDS window (< kWin - phase).  Each owner
+// lane first publishes its frame offset and the 16-bit byte masks of its 8 window
+// chunks (W.pref / W.s, W.e, W.first, W.last: free once the stream is done); the
+// lane that stores chunk c = k*64 + lane then needs two LDS reads.  Stores: a full
+// chunk is one dwordx4, a full dword one dword, the rest byte by byte.
+__device__ __forceinline__ uint32_t range_mask16(int lo, int hi) {
+    const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
+    return h > l ? (((1u << h) - 1u) & ~((1u << l) - 1u)) : 0u;
 }
 
-// Store frame bytes [r0, r1) and [r2, r3) (frame-relative, per owning lane) from the
-// tile's LDS slots.  Ranges lie inside the LDS window (< kWin - phase).
-__device__ __forceinline__ void write_back(uint8_t* frames, const WaveScratch& W, int lane,
+__device__ __forceinline__ void write_back(uint8_t* frames, WaveScratch& W, int lane,
                                            uint32_t off, uint32_t r0, uint32_t r1, uint32_t r2,
                                            uint32_t r3) {
+    {
+        const int ph = (int)(off & 15u);
+        uint32_t M[4];
+#pragma unroll
+        for (int j = 0; j < kWinChunks; j += 2) {
+            const int b0 = 16 * j - ph, b1 = 16 * (j + 1) - ph;   // chunk starts, frame-relative
+            const uint32_t m0 = range_mask16((int)r0 - b0, (int)r1 - b0) |
+                                range_mask16((int)r2 - b0, (int)r3 - b0);
+            const uint32_t m1 = range_mask16((int)r0 - b1, (int)r1 - b1) |
+                                range_mask16((int)r2 - b1, (int)r3 - b1);
+            M[j / 2] = m0 | (m1 << 16);
+        }
+        W.s[lane] = M[0];
+        W.e[lane] = M[1];
+        W.first[lane] = M[2];
+        W.last[lane] = M[3];
+        W.pref[lane] = off;
+    }
+    wave_sync();
 #pragma unroll
     for (int k = 0; k < kWinChunks; ++k) {
         const int c = k * kWave + lane;
         const int q = c / kWinChunks, j = c % kWinChunks;
-        const uint32_t qo = (uint32_t)__shfl((int)off, q, kWave);
-        const uint32_t a0 = (uint32_t)__shfl((int)r0, q, kWave), a1 = (uint32_t)__shfl((int)r1, q, kWave);
-        const uint32_t a2 = (uint32_t)__shfl((int)r2, q, kWave), a3 = (uint32_t)__shfl((int)r3, q, kWave);
-        const uint32_t base = (qo & ~15u) + 16u * j;         // chunk's absolute address
-        // chunk-relative byte mask of the two ranges
-        uint32_t m = 0;
-        {
-            const int lo = (int)(qo + a0) - (int)base, hi = (int)(qo + a1) - (int)base;
-            const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
-            if (h > l) m |= ((1u << h) - 1u) & ~((1u << l) - 1u);
-        }
-        {
-            const int lo = (int)(qo + a2) - (int)base, hi = (int)(qo + a3) - (int)base;
-            const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
-            if (h > l) m |= ((1u << h) - 1u) & ~((1u << l) - 1u);
-        }
+        const uint32_t mw = (j / 2 == 0) ? W.s[q] : (j / 2 == 1) ? W.e[q]
+                          : (j / 2 == 2) ? W.first[q] : W.last[q];
+        const uint32_t m = (mw >> (16 * (j & 1))) & 0xffffu;
         if (!m) continue;
-        const uint8_t* src = &W.win[q * kSlot + 16 * j];
+        const uint32_t base = (W.pref[q] & ~15u) + 16u * j;        // chunk's absolute address
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&W.win[q * kSlot + 16 * j]);
         if (m == 0xffffu) {
-            const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-            *reinterpret_cast<u32x4*>(frames + base) = u32x4{s4[0], s4[1], s4[2], s4[3]};
-        } else {
-            for (int b = 0; b < 16; ++b)
-                if (m & (1u << b)) frames[base + b] = src[b];
+            *reinterpret_cast<u32x4*>(frames + base) = u32x4{src[0], src[1], src[2], src[3]};
+            continue;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint32_t dm = (m >> (4 * d)) & 15u;
+            if (dm == 15u) {
+                *reinterpret_cast<uint32_t*>(frames + base + 4 * d) = src[d];
+            } else if (dm) {
+                const uint32_t v = src[d];
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (dm & (1u << b)) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
+            }
         }
     }
+}
+
+// Records of the tile, coalesced: 5 dwordx4 per lane over the tile's contiguous
+// 5 KiB, staged through the window area (stride 21 dwords), then each lane takes its
+// own 20 words.  Must run before the window is committed to LDS.
+__device__ __forceinline__ void load_records_tile(const rpkt_rec_t* recs, uint32_t p0, uint32_t n,
+                                                  WaveScratch& W, int lane, uint32_t (&w)[20]) {
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    const u32x4* in = reinterpret_cast<const u32x4*>(recs + p0);
+    u32x4 v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane;
+        v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+    }
+    uint32_t* st = rec_stage(W);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+        uint32_t* d = st + r * 21 + pc * 4;
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = st[lane * 21 + k];
+    wave_sync();
+}
+
+// End (frame-relative) of the range to write back for headers ending at `hdr_end`:
+// extended, with the window's original bytes, to the end of the 128-B cache line
+// (partially written lines cost the memory side a read-modify-write), clipped to the
+// frame and to the LDS window.
+__device__ __forceinline__ uint32_t line_end(Frame fr, uint32_t hdr_end) {
+    const uint32_t ph = fr.off & 15u;
+    const uint32_t line = ((fr.off + hdr_end + 127u) & ~127u) - fr.off;
+    uint32_t e = line < fr.len ? line : fr.len;
+    return e < kWin - ph ? e : kWin - ph;
 }
 
 // rpkt_gpu_build_batch: window -> headers composed in LDS -> checksums (IPv4 over the
@@ -1224,16 +1277,14 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
     const Frame fr = spans.get(i);
+    uint32_t w[20];
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
         const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        load_records_tile(recs, p0, n, W, lane, w);             // window loads in flight
         window_commit(W, rs, fb, d, addr, fix, lane);
     }
-    uint32_t w[20];
-#pragma unroll
-    for (int k = 0; k < 20; ++k) w[k] = 0;
-    if (valid) load_record(recs, i, w);
     wave_sync();
 
     const uint32_t ph = fr.off & 15u, len = fr.len;
@@ -1290,19 +1341,24 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         }
     }
     wave_sync();
-    write_back(frames, W, lane, fr.off, 0u, ok ? l4 + fixed4 : 0u, 0u, 0u);
+    // the window holds the original bytes around the headers: round the written range
+    // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
+    const uint32_t r1 = ok ? line_end(fr, l4 + fixed4) : 0u;
+    write_back(frames, W, lane, fr.off, 0u, r1, 0u, 0u);
     if (built && valid) built[i] = ok ? 1 : 0;
 }
 
-// rpkt_gpu_forward_batch: record -> verdict -> rewritten fixed headers.  Checksums are
-// updated from the record's verify sums (RFC 1624): swapping addresses and ports
-// leaves every one's-complement sum unchanged, so only the TTL word and the zeroed
-// checksum field move the sum; both sums are of non-zero data, hence equal to a full
-// recompute bit for bit (tests compare with the oracle's full recompute).
-__global__ __launch_bounds__(kWave * kWavesPerBlock)
+// rpkt_gpu_forward_batch: the loopback_rx loop fused into one pass per frame: header
+// window -> parse (both sums) -> RX verdict -> rewrite in the LDS window -> write-back.
+// Checksums are updated from the verify sums (RFC 1624): swapping addresses and
+// ports leaves every one's-complement sum unchanged, so only the TTL word and the
+// zeroed checksum field move it; both sums are of non-zero data, hence equal to a
+// full recompute bit for bit (the oracle recomputes in full).  The written range is
+// rounded up to whole 16-B chunks inside the frame (the window holds the original
+// payload bytes), so a 64-B frame is rewritten with three dwordx4 stores.
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
 void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
-                    uint32_t stride, uint32_t frame_len, uint32_t n,
-                    const rpkt_rec_t* __restrict__ recs, rpkt_fwd_t fwd,
+                    uint32_t stride, uint32_t frame_len, uint32_t n, rpkt_fwd_t fwd,
                     uint8_t* __restrict__ keep) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1);
@@ -1312,54 +1368,319 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     if (p0 >= n) return;
     const uint32_t i = p0 + lane;
     const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
     const Frame fr = spans.get(i);
-    uint32_t w[20];
-#pragma unroll
-    for (int k = 0; k < 20; ++k) w[k] = 0;
-    if (valid) load_record(recs, i, w);
-    const uint32_t l3 = w[16] & 0xffffu, l4 = w[16] >> 16;
-    const uint32_t ip_sum = w[18] & 0xffffu, l4_sum = w[18] >> 16;
-    const uint32_t udp_ck = w[15] & 0xffffu;
-    // untagged IPv4 (w0 = status | n_vlan << 8 | ethertype << 16), UDP, sums valid
-    bool fwd_ok = valid && (w[0] & 0xffffu) == RPKT_S_OK && (w[0] >> 16) == 0x0800u &&
-             ip_sum == 0xffffu && ((w[8] >> 8) & 0xffu) == 17u &&
-             (l4_sum == 0xffffu || udp_ck == 0u) && fr.len >= l4 + 8u;
-    if (fwd_ok && fwd.n_forbid) {                               // sorted: binary search
-        uint32_t lo = 0, hi = fwd.n_forbid;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (fwd.forbid_dev[mid] < w[9]) lo = mid + 1; else hi = mid;
-        }
-        if (lo < fwd.n_forbid && fwd.forbid_dev[lo] == w[9]) fwd_ok = false;
-    }
-    uint32_t r1 = 0, r2 = 0, r3 = 0;
-    if (fwd_ok) {
-        const uint32_t ttl = w[8] & 0xffu, proto = 17u;
-        const uint32_t old_w = (ttl << 8) | proto, new_w = (((ttl - 1u) & 0xffu) << 8) | proto;
-        const uint32_t ip_ck = ~fold16(ip_sum + (~(w[8] >> 16) & 0xffffu) + (~old_w & 0xffffu) +
-                                       new_w) & 0xffffu;
-        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu)) & 0xffffu;
-        if (u_ck == 0u) u_ck = 0xffffu;
-        uint32_t m[20];
-#pragma unroll
-        for (int k = 0; k < 20; ++k) m[k] = w[k];
-        m[1] = fwd.dmac[0] | (fwd.dmac[1] << 8) | (fwd.dmac[2] << 16) | (fwd.dmac[3] << 24);
-        m[2] = fwd.dmac[4] | (fwd.dmac[5] << 8) | (fwd.smac[0] << 16) | (fwd.smac[1] << 24);
-        m[3] = fwd.smac[2] | (fwd.smac[3] << 8) | (fwd.smac[4] << 16) | (fwd.smac[5] << 24);
-        m[8] = (w[8] & ~0xffu) | ((ttl - 1u) & 0xffu);       // ttl - 1, wrapping
-        m[9] = w[10];
-        m[10] = w[9];
-        m[11] = (w[11] >> 16) | (w[11] << 16);
-        emit_headers(&W.win[lane * kSlot] + (fr.off & 15u), m, 0u, l3, l4, proto, w[6] >> 16,
-                     w[14] & 0xffffu, ip_ck, u_ck);
-        r1 = l3 + 20u;
-        r2 = l4;
-        r3 = l4 + 8u;
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
     }
     wave_sync();
-    write_back(frames, W, lane, fr.off, 0u, r1, r2, r3);
+    LaneRec L;
+    parse_lane(W, lane, fr, valid, RPKT_F_IP_SUM | RPKT_F_L4_SUM, L);
+    uint8_t* slot = &W.win[lane * kSlot];
+    uint8_t* s = slot + (fr.off & 15u);
+    {
+        // loopback_rx.rs:99-106 before the L4 sum is known: Ok chain, untagged IPv4
+        // (w0 = status | n_vlan << 8 | ethertype << 16), IP checksum good, UDP.  The
+        // rewrite that does not depend on the L4 sum is done in the window now
+        // (written back only if the frame is kept); what the rest needs waits in the
+        // slot's spare dword: pre | l4 << 8 | udp checksum << 16.
+        const uint32_t w0 = L.w[0], w8 = L.w[8], w9 = L.w[9], w10 = L.w[10], w11 = L.w[11];
+        const uint32_t ip_sum = L.w[18] & 0xffffu, l4 = L.w[16] >> 16;
+        const bool pre = valid && (w0 & 0xffffu) == RPKT_S_OK && (w0 >> 16) == 0x0800u &&
+                         ip_sum == 0xffffu && ((w8 >> 8) & 0xffu) == 17u;
+        if (pre) {                                              // loopback_rx.rs:120-133
+            const uint32_t ttl = w8 & 0xffu;
+            const uint32_t old_w = (ttl << 8) | 17u, new_w = (((ttl - 1u) & 0xffu) << 8) | 17u;
+            const uint32_t ip_ck = ~fold16(ip_sum + (~(w8 >> 16) & 0xffffu) +
+                                           (~old_w & 0xffffu) + new_w) & 0xffffu;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                s[k] = fwd.dmac[k];
+                s[6 + k] = fwd.smac[k];
+            }
+            s[22] = (uint8_t)(ttl - 1u);
+            put_be16(s + 24, ip_ck);
+            put_be32(s + 26, w10);
+            put_be32(s + 30, w9);
+            put_be16(s + l4, w11 >> 16);
+            put_be16(s + l4 + 2, w11);
+        }
+        *reinterpret_cast<uint32_t*>(slot + kWin) =
+            (uint32_t)pre | (l4 << 8) | ((L.w[15] & 0xffffu) << 16);
+    }
+    const uint32_t sp = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
+    const uint32_t l4_sum =
+        L.want_l4 ? fold16(L.pseudo + be_sum(L.l4_part + sp, L.l4_start_abs)) : 0u;
+    const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
+    const uint32_t l4 = (info >> 8) & 0xffu, udp_ck = info >> 16;
+    bool fwd_ok = (info & 1u) && (l4_sum == 0xffffu || udp_ck == 0u);   // :107 L4 good
+    if (fwd.n_forbid) {                                         // :111-118, sorted list
+        // up to 128 addresses are searched in LDS (W.s and W.e, contiguous, free once
+        // the stream is done), a longer list in global memory
+        const bool in_lds = fwd.n_forbid <= 2u * kWave;
+        const uint32_t* list = fwd.forbid_dev;
+        if (in_lds) {
+            uint32_t* t = W.s;
+            if ((uint32_t)lane < fwd.n_forbid) t[lane] = fwd.forbid_dev[lane];
+            if ((uint32_t)lane + kWave < fwd.n_forbid) t[lane + kWave] = fwd.forbid_dev[lane + kWave];
+            wave_sync();
+            list = t;
+        }
+        if (fwd_ok) {
+            const uint32_t src = ((uint32_t)s[30] << 24) | ((uint32_t)s[31] << 16) |
+                                 ((uint32_t)s[32] << 8) | s[33];   // swapped: old source
+            uint32_t lo = 0, hi = fwd.n_forbid;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (list[mid] < src) lo = mid + 1; else hi = mid;
+            }
+            if (lo < fwd.n_forbid && list[lo] == src) fwd_ok = false;
+        }
+        wave_sync();
+    }
+    uint32_t r1 = 0;
+    if (fwd_ok) {
+        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu)) & 0xffffu;
+        if (u_ck == 0u) u_ck = 0xffffu;                         // RFC 768
+        put_be16(s + l4 + 6, u_ck);
+        r1 = line_end(fr, l4 + 8u);
+    }
+    wave_sync();
+    write_back(frames, W, lane, fr.off, 0u, r1, 0u, 0u);
     if (valid) keep[i] = fwd_ok ? 1 : 0;
+}
+
+// ---- option iterators: TcpOptionsIter / Ipv4OptionsIter over a parsed batch ----
+// One wave per 64 frames.  The records give each frame's option slices; only the
+// 16-B chunks that overlap a slice are loaded (frames without options cost their
+// record read and the 64-B output only).  Lane-per-frame walk over LDS bytes with
+// the per-type parse rules of the generated option views (oracle/rpkt_oracle_opts.c
+// cites them); results staged through LDS and stored as 4 KiB of coalesced rows.
+constexpr int kOptChunks = 10;                 // 160 B from the frame's 16-B phase:
+constexpr int kOptSlot = 164;                  // covers l4 + doff*4 <= 142 at any phase
+struct OptScratch {
+    uint8_t win[kWave * kOptSlot];             // 10 496 B (stride 41 dwords: conflict-free)
+};
+static_assert(kWave * 21 * 4 <= kWave * kOptSlot, "record stage fits the option window");
+
+__device__ __forceinline__ uint32_t lds8(const uint8_t* p, uint32_t a) { return p[a]; }
+
+// returns option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown
+__device__ __forceinline__ int tcp_opt_len(const uint8_t* s, uint32_t at, uint32_t n, int& kind) {
+    const uint32_t t = lds8(s, at), hl = n >= 2 ? lds8(s, at + 1) : 0u;
+    switch (t) {
+        case 0: kind = 0; return 1;
+        case 1: kind = 1; return 1;
+        case 2: kind = 2; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 3: kind = 3; return (n >= 3 && hl == 3) ? 3 : 0;
+        case 4: kind = 4; return (n >= 2 && hl == 2) ? 2 : 0;
+        case 5: kind = 5; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        case 8: kind = 6; return (n >= 10 && hl == 10) ? 10 : 0;
+        case 34: kind = 7; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        default: return -1;
+    }
+}
+__device__ __forceinline__ int ip_opt_len(const uint8_t* s, uint32_t at, uint32_t n, int& kind) {
+    const uint32_t t = lds8(s, at), hl = n >= 2 ? lds8(s, at + 1) : 0u;
+    switch (t) {
+        case 0: kind = 0; return 1;
+        case 1: kind = 1; return 1;
+        case 68: kind = 2; return (n >= 4 && hl >= 4 && hl <= n) ? (int)hl : 0;
+        case 7: kind = 3; return (n >= 3 && hl >= 3 && hl <= n) ? (int)hl : 0;
+        case 148: kind = 4; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 134: kind = 5; return (n >= 6 && hl >= 6 && hl <= n) ? (int)hl : 0;
+        case 137: kind = 6; return (n >= 7 && hl == 7) ? 7 : 0;
+        case 131: kind = 7; return (n >= 7 && hl == 7) ? 7 : 0;
+        default: return -1;
+    }
+}
+__device__ __forceinline__ uint32_t lds_be16(const uint8_t* s, uint32_t a) {
+    return (lds8(s, a) << 8) | lds8(s, a + 1);
+}
+__device__ __forceinline__ uint32_t lds_be32(const uint8_t* s, uint32_t a) {
+    return (lds8(s, a) << 24) | (lds8(s, a + 1) << 16) | (lds8(s, a + 2) << 8) | lds8(s, a + 3);
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
+                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                    uint32_t n, const rpkt_rec_t* __restrict__ recs, rpkt_opts_t* __restrict__ opts) {
+    __shared__ __attribute__((aligned(16))) OptScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    OptScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+
+    // records of the tile (coalesced), keep the four words the walks need
+    uint32_t w0, w8, w14, w16;
+    {
+        const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+        const u32x4* in = reinterpret_cast<const u32x4*>(recs + p0);
+        u32x4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t c = k * kWave + lane;
+            v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+        }
+        uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+            uint32_t* d = st + r * 21 + pc * 4;
+            d[0] = v[k].x;
+            d[1] = v[k].y;
+            d[2] = v[k].z;
+            d[3] = v[k].w;
+        }
+        wave_sync();
+        w0 = st[lane * 21 + 0];
+        w8 = st[lane * 21 + 8];
+        w14 = st[lane * 21 + 14];
+        w16 = st[lane * 21 + 16];
+        wave_sync();
+    }
+    const uint32_t status = w0 & 0xffu;
+    const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
+    const bool tcp = status == RPKT_S_OK && ((w8 >> 8) & 0xffu) == 6u;
+    const uint32_t l3 = w16 & 0xffffu, l4 = w16 >> 16;
+    const uint32_t ip_lo = l3 + 20u, ip_hi = ip_parsed ? l4 : ip_lo;
+    const uint32_t t_lo = l4 + 20u, t_hi = tcp ? l4 + ((w14 >> 12) & 0xfu) * 4u : t_lo;
+    // option bytes needed: [lo, hi) of the frame (both slices); chunks outside it skip
+    const uint32_t need_lo = ip_hi > ip_lo ? ip_lo : t_lo;
+    const uint32_t need_hi = t_hi > t_lo ? t_hi : ip_hi;
+    const bool need = (ip_hi > ip_lo) || (t_hi > t_lo);
+
+    // window chunks that overlap the option bytes -> LDS slots
+    {
+        u32x4 d[kOptChunks];
+        uint32_t addr[kOptChunks];
+        uint32_t fix = 0;
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) {
+            const int c = k * kWave + lane;
+            const int q = c / kOptChunks, j = c % kOptChunks;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t lo = (uint32_t)__shfl((int)(need ? fr.off + need_lo : 0u), q, kWave);
+            const uint32_t hi = (uint32_t)__shfl((int)(need ? fr.off + need_hi : 0u), q, kWave);
+            const uint32_t a = (qo & ~15u) + 16u * j;
+            addr[k] = (a < hi && a + 16u > lo) ? a : fb;
+            fix |= (uint32_t)straddles(addr[k], fb) << k;
+        }
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) {
+            const int c = k * kWave + lane;
+            u32x4 v = d[k];
+            if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kOptChunks) * kOptSlot +
+                                                              (c % kOptChunks) * 16]);
+            dst[0] = v.x;
+            dst[1] = v.y;
+            dst[2] = v.z;
+            dst[3] = v.w;
+        }
+    }
+    wave_sync();
+
+    // the two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
+    // TcpOptionsIter::next, tcp/generated.rs:1400-1484)
+    const uint8_t* s = &W.win[lane * kOptSlot] + (fr.off & 15u);
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    uint64_t ip_trace = 0, tcp_trace = 0;
+    if (ip_parsed) {
+        uint32_t pos = 0, cnt = 0, kinds = 0, stop = RPKT_OPT_END;
+        const uint32_t nb = ip_hi - ip_lo;
+        while (pos < nb) {
+            int kind = 0;
+            const int used = ip_opt_len(s, ip_lo + pos, nb - pos, kind);
+            if (used <= 0) {
+                stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                break;
+            }
+            const uint32_t at = ip_lo + pos;
+            if (kind == 2) o[9] = (o[9] & 0xff000000u) | lds8(s, at + 1) |
+                                  (lds8(s, at + 2) << 8) | (lds8(s, at + 3) << 16);
+            if (kind == 3) o[8] = (o[8] & 0xffffu) | (lds8(s, at + 1) << 16) | (lds8(s, at + 2) << 24);
+            if (kind == 4) o[8] = (o[8] & 0xffff0000u) | lds_be16(s, at + 2);
+            if (kind == 5) o[11] = lds_be32(s, at + 2);
+            if (kind == 6 || kind == 7) {
+                o[9] = (o[9] & 0x00ffffffu) | (lds8(s, at + 2) << 24);
+                o[10] = lds_be32(s, at + 3);
+            }
+            kinds |= 1u << kind;
+            if (cnt < 16) ip_trace |= (uint64_t)(kind + 1) << (4 * cnt);
+            cnt += 1;
+            pos += (uint32_t)used;
+        }
+        // word 6: tcp_fo_len | tcp_end << 16 | ip_end << 24; word 7: ip_count | ip_stop << 8 | ip_kinds << 16
+        o[6] |= pos << 24;
+        o[7] = cnt | (stop << 8) | (kinds << 16);
+    }
+    if (tcp) {
+        uint32_t pos = 0, cnt = 0, kinds = 0, stop = RPKT_OPT_END;
+        const uint32_t nb = t_hi - t_lo;
+        while (pos < nb) {
+            int kind = 0;
+            const int used = tcp_opt_len(s, t_lo + pos, nb - pos, kind);
+            if (used <= 0) {
+                stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                break;
+            }
+            const uint32_t at = t_lo + pos;
+            if (kind == 2) o[1] = (o[1] & 0xffffu) | (lds_be16(s, at + 2) << 16);
+            if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (lds8(s, at + 2) << 16);
+            if (kind == 5) {
+                const uint32_t hl = lds8(s, at + 1);
+                o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
+                o[4] = hl >= 6u ? lds_be32(s, at + 2) : 0u;
+                o[5] = hl >= 10u ? lds_be32(s, at + 6) : 0u;
+            }
+            if (kind == 6) {
+                o[2] = lds_be32(s, at + 2);
+                o[3] = lds_be32(s, at + 6);
+            }
+            if (kind == 7) o[6] = (o[6] & 0xffff0000u) | lds8(s, at + 1);
+            kinds |= 1u << kind;
+            if (cnt < 16) tcp_trace |= (uint64_t)(kind + 1) << (4 * cnt);
+            cnt += 1;
+            pos += (uint32_t)used;
+        }
+        // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24; word 1: kinds | mss << 16
+        o[0] = (o[0] & 0xffff0000u) | cnt | (stop << 8);
+        o[1] = (o[1] & 0xffff0000u) | kinds;
+        o[6] = (o[6] & 0xff00ffffu) | (pos << 16);
+    }
+    o[12] = (uint32_t)tcp_trace;
+    o[13] = (uint32_t)(tcp_trace >> 32);
+    o[14] = (uint32_t)ip_trace;
+    o[15] = (uint32_t)(ip_trace >> 32);
+
+    // stage (stride 17 dwords) and store 64 rows of 64 B coalesced
+    wave_sync();
+    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[c]);
+    }
 }
 
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
@@ -1714,21 +2035,36 @@ int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint
                   b->stride, flen, b->n, recs_dev, flags, built_dev);
 }
 
-int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
-                           const rpkt_fwd_t* fwd, uint8_t* keep_dev, void* stream) {
-    if (!b || !recs_dev || !fwd || !keep_dev) return RPKT_E_INVAL;
+int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
+                           void* stream) {
+    if (!b || !fwd || !keep_dev) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev || (fwd->n_forbid && !fwd->forbid_dev)) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
-    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)b->frames_dev & 15u) != 0)
-        return RPKT_E_ALIGN;
+    if (((uintptr_t)b->frames_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     return launch(forward_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
-                  b->stride, flen, b->n, recs_dev, *fwd, keep_dev);
+                  b->stride, flen, b->n, *fwd, keep_dev);
+}
+
+int rpkt_gpu_options_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
+                           rpkt_opts_t* opts_dev, void* stream) {
+    if (!b || !recs_dev || !opts_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(options_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  recs_dev, opts_dev);
 }
 
 // Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from .build import GPU_LIB
-from .records import REC_BYTES, F_FLOW_EV
+from .records import OPTS_BYTES, REC_BYTES, F_FLOW_EV
 
 RPKT_OK = 0
 ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN"}
@@ -47,7 +47,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_last_hip_error", "rpkt_gpu_device_info", "rpkt_gpu_parse_batch", "rpkt_gpu_flow_workspace_bytes",
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
-           "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch"]
+           "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
+           "rpkt_gpu_options_batch"]
 
 _lib = None
 
@@ -96,9 +97,12 @@ def lib():
         L.rpkt_gpu_build_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_build_batch.restype = ctypes.c_int
-        L.rpkt_gpu_forward_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
-                                             ctypes.POINTER(Fwd), ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_forward_batch.argtypes = [ctypes.POINTER(Batch), ctypes.POINTER(Fwd),
+                                             ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_forward_batch.restype = ctypes.c_int
+        L.rpkt_gpu_options_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_options_batch.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -286,8 +290,8 @@ def build_batch(batch, recs, flags=3, built=None, stream=None):
     return built
 
 
-def forward_batch(batch, recs, dmac, smac, forbid=None, keep=None, stream=None):
-    """rpkt_gpu_forward_batch (loopback_rx firewall rewrite) over a parsed batch.
+def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None):
+    """rpkt_gpu_forward_batch (loopback_rx firewall: parse, verdict, rewrite in place).
     forbid: int64 tensor of IPv4 addresses (host-order u32 values) on the device."""
     torch = _torch()
     if keep is None:
@@ -300,7 +304,20 @@ def forward_batch(batch, recs, dmac, smac, forbid=None, keep=None, stream=None):
         forbid = u32.to(torch.int32)                                         # same bits
         f.forbid_dev, f.n_forbid = forbid.data_ptr(), forbid.numel()
     d = batch.desc()
-    rc = lib().rpkt_gpu_forward_batch(ctypes.byref(d), recs.data_ptr(), ctypes.byref(f),
-                                      keep.data_ptr(), _stream_ptr(stream))
+    rc = lib().rpkt_gpu_forward_batch(ctypes.byref(d), ctypes.byref(f), keep.data_ptr(),
+                                      _stream_ptr(stream))
     _check(rc, "rpkt_gpu_forward_batch")
     return keep
+
+
+def options_batch(batch, recs, opts=None, stream=None):
+    """rpkt_gpu_options_batch: IPv4 and TCP option walks of a parsed batch
+    (recs from parse_batch); returns the uint8 tensor of n * 64-byte rpkt_opts_t."""
+    torch = _torch()
+    if opts is None:
+        opts = torch.empty(batch.n * OPTS_BYTES, dtype=torch.uint8, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_options_batch(ctypes.byref(d), recs.data_ptr(), opts.data_ptr(),
+                                      _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_options_batch")
+    return opts

@@ -35,6 +35,35 @@ MAX_VLAN = 2
 FLOW_MAX_BUCKETS = 65535
 
 
+OPTS_BYTES = 64
+OPTS_DTYPE = np.dtype([          # rpkt_opts_t (include/rpkt_gpu.h), 64 B
+    ("tcp_count", "u1"), ("tcp_stop", "u1"), ("tcp_wscale", "u1"), ("tcp_sack_blocks", "u1"),
+    ("tcp_kinds", "<u2"), ("tcp_mss", "<u2"), ("tcp_ts", "<u4"), ("tcp_ts_echo", "<u4"),
+    ("tcp_sack_left", "<u4"), ("tcp_sack_right", "<u4"), ("tcp_fo_len", "<u2"),
+    ("tcp_end", "u1"), ("ip_end", "u1"), ("ip_count", "u1"), ("ip_stop", "u1"),
+    ("ip_kinds", "<u2"), ("ip_route_alert", "<u2"), ("ip_rr_len", "u1"), ("ip_rr_pointer", "u1"),
+    ("ip_ts_len", "u1"), ("ip_ts_pointer", "u1"), ("ip_ts_oflw_flg", "u1"),
+    ("ip_sr_pointer", "u1"), ("ip_sr_dest", "<u4"), ("ip_cs_doi", "<u4"),
+    ("tcp_trace", "<u8"), ("ip_trace", "<u8"),
+])
+assert OPTS_DTYPE.itemsize == OPTS_BYTES
+OPT_STOP = {"NONE": 0, "END": 1, "UNKNOWN": 2, "MALFORMED": 3}
+TCP_KINDS = ("Eol", "Nop", "Mss", "WindowScale", "SackPermitted", "Sack", "Timestamp", "FastOpen")
+IP_KINDS = ("Eol", "Nop", "Timestamp", "RecordRoute", "RouteAlert", "CommercialSecurity",
+            "StrictSourceRoute", "LooseSourceRoute")
+
+
+def trace_kinds(trace, count, names):
+    """The first min(count, 16) option kinds of a *_trace field, by name."""
+    return [names[((int(trace) >> (4 * k)) & 15) - 1] for k in range(min(int(count), 16))]
+
+
+def as_opts(raw):
+    """View a uint8 buffer of n * 64 bytes as rpkt_opts_t records."""
+    a = np.ascontiguousarray(raw).view(np.uint8)
+    return a.view(OPTS_DTYPE)
+
+
 def as_records(raw):
     """View a uint8 buffer of n*80 bytes (numpy or CPU torch) as a record array."""
     a = np.asarray(raw)

@@ -44,12 +44,25 @@ def test_status_names_match_records(L):
     assert L.rpkt_gpu_status_name(99) == b"?"
 
 
+def struct_offsets(src, name):
+    """Offsets in the `/* NN` comments of one typedef struct of the header."""
+    body = src[src.index("typedef struct %s {" % name):]
+    body = body[:body.index("}")]
+    return [int(m) for m in re.findall(r";\s*/\*\s*(\d+) ", body)]
+
+
 def test_record_layout_matches_header():
     src = open(HDR).read()
-    fields = re.findall(r"/\*\s*(\d+)\s*(?:enum|[a-z]|\s)", src)
-    offs = [int(m) for m in re.findall(r";\s*/\*\s*(\d+) ", src)]
+    offs = struct_offsets(src, "rpkt_rec")
     assert offs == [records.REC_DTYPE.fields[n][1] for n in records.REC_DTYPE.names]
-    assert records.REC_BYTES == 80 and fields
+    assert records.REC_BYTES == 80
+
+
+def test_opts_layout_matches_header():
+    src = open(HDR).read()
+    offs = struct_offsets(src, "rpkt_opts")
+    assert offs == [records.OPTS_DTYPE.fields[n][1] for n in records.OPTS_DTYPE.names]
+    assert records.OPTS_BYTES == 64
 
 
 def test_flow_hash_matches_oracle(L):

@@ -101,10 +101,9 @@ def test_forward_parity(torch, cfg):
     n = {2: 1 << 20, 4: 1 << 20, 6: 1 << 16}[cfg]
     hb = gen.make_batch(cfg, n, seed=400 + cfg)
     db = engine.DeviceBatch.from_host(hb)
-    recs = engine.parse_batch(db, 3)
-    r = as_records(recs.cpu().numpy())
+    r = as_records(engine.parse_batch(db, 3).cpu().numpy())
     forbid = np.unique(r["ip_src"][::97])[:64].astype(np.int64)
-    keep = engine.forward_batch(db, recs, DMAC, SMAC, torch.from_numpy(forbid).cuda())
+    keep = engine.forward_batch(db, DMAC, SMAC, torch.from_numpy(forbid).cuda())
     o, ok = oracle.forward_batch(hb.frames, hb.n, r, DMAC, SMAC, forbid.astype(np.uint32),
                                  offsets=hb.offsets, stride=hb.stride, frame_len=hb.frame_len)
     assert np.array_equal(keep.cpu().numpy(), ok)
@@ -114,12 +113,26 @@ def test_forward_parity(torch, cfg):
         assert 0.3 < ok.mean() < 0.999
 
 
+def test_forward_long_forbid_list(torch):
+    """More than 128 forbidden addresses: the binary search runs in global memory."""
+    hb = gen.make_batch(2, 1 << 16, seed=12)
+    db = engine.DeviceBatch.from_host(hb)
+    r = as_records(engine.parse_batch(db, 3).cpu().numpy())
+    forbid = np.unique(np.concatenate([r["ip_src"][::50], np.arange(1000, 1400)])).astype(np.int64)
+    assert forbid.size > 128
+    keep = engine.forward_batch(db, DMAC, SMAC, torch.from_numpy(forbid).cuda()).cpu().numpy()
+    o, ok = oracle.forward_batch(hb.frames, hb.n, r, DMAC, SMAC, forbid.astype(np.uint32),
+                                 stride=hb.stride)
+    assert np.array_equal(keep, ok)
+    assert np.array_equal(db.frames.cpu().numpy(), o)
+
+
 def test_forward_empty_forbid_and_rejects(torch):
     hb = gen.make_batch(2, 4096, seed=9)
     db = engine.DeviceBatch.from_host(hb)
     recs = engine.parse_batch(db, 3)
-    keep = engine.forward_batch(db, recs, DMAC, SMAC, None).cpu().numpy()
     r = as_records(recs.cpu().numpy())
+    keep = engine.forward_batch(db, DMAC, SMAC, None).cpu().numpy()
     assert np.array_equal(keep.astype(bool), r["ip_sum"] == 0xFFFF)
     with pytest.raises(engine.RpktError):
         engine.build_batch(db, recs, flags=4)
