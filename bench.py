@@ -336,7 +336,7 @@ def run_tx(cfg, mode, args, rank, world):
     recs = [engine.parse_batch(db, 3) for db in dbs]
     outs = [torch.empty(hb.n * (64 if mode == "opts" else 1), dtype=torch.uint8, device="cuda")
             for hb in hbs]
-    forbid = torch.tensor([ip_u32(x) for x in FORBID_IPS], dtype=torch.int64, device="cuda")
+    forbid = engine.forbid_list([ip_u32(x) for x in FORBID_IPS])
     dmac, smac = bytes([0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]), bytes([0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6])
     stream = torch.cuda.current_stream()
 

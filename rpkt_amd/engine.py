@@ -290,9 +290,17 @@ def build_batch(batch, recs, flags=3, built=None, stream=None):
     return built
 
 
+def forbid_list(addrs, device="cuda"):
+    """Device copy of a forbidden-source list for forward_batch: IPv4 addresses as
+    host-order u32 values, sorted ascending (the C ABI's binary search), int32 bits."""
+    torch = _torch()
+    a = np.unique(np.asarray(addrs, dtype=np.int64) & 0xFFFFFFFF).astype(np.uint32)
+    return torch.from_numpy(a.view(np.int32).copy()).to(device)
+
+
 def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None):
     """rpkt_gpu_forward_batch (loopback_rx firewall: parse, verdict, rewrite in place).
-    forbid: int64 tensor of IPv4 addresses (host-order u32 values) on the device."""
+    forbid: None or a tensor from forbid_list()."""
     torch = _torch()
     if keep is None:
         keep = torch.empty(batch.n, dtype=torch.uint8, device=batch.frames.device)
@@ -300,8 +308,8 @@ def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None):
     f.dmac[:] = list(bytes(dmac))
     f.smac[:] = list(bytes(smac))
     if forbid is not None and forbid.numel():
-        u32 = torch.sort(forbid.to(torch.int64) & 0xFFFFFFFF).values      # u32 order
-        forbid = u32.to(torch.int32)                                         # same bits
+        if forbid.dtype != torch.int32:
+            raise RpktError("forbid must come from forbid_list() (sorted u32 as int32)")
         f.forbid_dev, f.n_forbid = forbid.data_ptr(), forbid.numel()
     d = batch.desc()
     rc = lib().rpkt_gpu_forward_batch(ctypes.byref(d), ctypes.byref(f), keep.data_ptr(),

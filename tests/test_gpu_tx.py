@@ -103,7 +103,7 @@ def test_forward_parity(torch, cfg):
     db = engine.DeviceBatch.from_host(hb)
     r = as_records(engine.parse_batch(db, 3).cpu().numpy())
     forbid = np.unique(r["ip_src"][::97])[:64].astype(np.int64)
-    keep = engine.forward_batch(db, DMAC, SMAC, torch.from_numpy(forbid).cuda())
+    keep = engine.forward_batch(db, DMAC, SMAC, engine.forbid_list(forbid))
     o, ok = oracle.forward_batch(hb.frames, hb.n, r, DMAC, SMAC, forbid.astype(np.uint32),
                                  offsets=hb.offsets, stride=hb.stride, frame_len=hb.frame_len)
     assert np.array_equal(keep.cpu().numpy(), ok)
@@ -120,7 +120,7 @@ def test_forward_long_forbid_list(torch):
     r = as_records(engine.parse_batch(db, 3).cpu().numpy())
     forbid = np.unique(np.concatenate([r["ip_src"][::50], np.arange(1000, 1400)])).astype(np.int64)
     assert forbid.size > 128
-    keep = engine.forward_batch(db, DMAC, SMAC, torch.from_numpy(forbid).cuda()).cpu().numpy()
+    keep = engine.forward_batch(db, DMAC, SMAC, engine.forbid_list(forbid)).cpu().numpy()
     o, ok = oracle.forward_batch(hb.frames, hb.n, r, DMAC, SMAC, forbid.astype(np.uint32),
                                  stride=hb.stride)
     assert np.array_equal(keep, ok)
