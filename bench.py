@@ -33,7 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from rpkt_amd import dist as rdist, engine, gen  # noqa: E402
-from rpkt_amd.records import REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
+from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -330,12 +330,15 @@ def run_tx(cfg, mode, args, rank, world):
     torch.cuda.empty_cache()
     n = args.frames or gen.DEFAULT_N[cfg]
     R = 4 if cfg == 2 else 1
-    hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
-           for r in range(R)]
+    if cfg == 9:                                   # protocol mix (captures + fuzz)
+        hbs = [gen.make_mix(n, seed=gen.DEFAULT_SEED[9] + 7919 * rank)]
+    else:
+        hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
+               for r in range(R)]
     dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
     recs = [engine.parse_batch(db, 3) for db in dbs]
-    outs = [torch.empty(hb.n * (64 if mode == "opts" else 1), dtype=torch.uint8, device="cuda")
-            for hb in hbs]
+    outs = [torch.empty(hb.n * (64 if mode in ("opts", "layers") else 1), dtype=torch.uint8,
+                        device="cuda") for hb in hbs]
     forbid = engine.forbid_list([ip_u32(x) for x in FORBID_IPS])
     dmac, smac = bytes([0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]), bytes([0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6])
     stream = torch.cuda.current_stream()
@@ -346,6 +349,8 @@ def run_tx(cfg, mode, args, rank, world):
             engine.build_batch(dbs[j], recs[j], 3, built=outs[j], stream=stream)
         elif mode == "opts":
             engine.options_batch(dbs[j], recs[j], opts=outs[j], stream=stream)
+        elif mode == "layers":
+            engine.layers_batch(dbs[j], out=outs[j], stream=stream)
         else:
             engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
 
@@ -371,6 +376,9 @@ def run_tx(cfg, mode, args, rank, world):
     fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
     if mode == "build":
         alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
+    elif mode == "layers":                     # header bytes walked + 64 B out per frame
+        lo = outs[0].cpu().numpy().view(LAYERS_DTYPE)
+        alg = int(np.minimum(lo["payload_off"].astype(np.int64), lens).sum()) + hbs[0].n * 64
     elif mode == "opts":                       # records + option slices read, 64 B written
         ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
@@ -390,6 +398,8 @@ def run_tx(cfg, mode, args, rank, world):
                      "fill" if mode == "build" else
                      "options: Ipv4OptionsIter + TcpOptionsIter walks of a parsed batch"
                      if mode == "opts" else
+                     "layers: pktfmt-derived protocol walk (captures mix, fuzzed)"
+                     if mode == "layers" else
                      "forward: loopback_rx firewall fused (parse + both sums, 8 forbidden "
                      "sources, swap + ttl-1 + MACs + checksum update)")}
 
@@ -406,7 +416,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tx", default="build2,build3,forward2,opts5",
+    ap.add_argument("--tx", default="build2,build3,forward2,opts5,layers9",
                     help="legs beyond the parse reported under 'extra' (build<cfg>, "
                          "forward<cfg>, opts<cfg>)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
@@ -431,7 +441,7 @@ def main():
         if c != args.config:
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
     for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
-        mode = next(m for m in ("build", "forward", "opts") if leg.startswith(m))
+        mode = next(m for m in ("build", "forward", "opts", "layers") if leg.startswith(m))
         extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
 
     if rank == 0:

@@ -28,6 +28,8 @@
 #define RPKT_GPU_H
 
 #include <stddef.h>
+
+#include "rpkt_protocols.h"
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -336,6 +338,42 @@ typedef struct rpkt_opts {
  * tcp: [l4 + 20, payload_off) for status OK / TCP).  opts_dev n * 64 B, 16-B aligned. */
 int rpkt_gpu_options_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
                            rpkt_opts_t* opts_dev, void* stream);
+
+/* ---- Protocol layer walk ---------------------------------------------------------- */
+
+/* The protocol stack of each frame, walked with the header views of every protocol
+ * rpkt generates from its pktfmt specs (include/rpkt_protocols.h): each layer is the
+ * protocol's group_parse / parse (the pktfmt codegen rules: header_len, payload_len /
+ * packet_len checks against chunk() and remaining()) and payload() (trim, advance).
+ * Which group follows a layer is the dispatch a receive loop writes by hand in the
+ * reference (ethertype, IP protocol / next header, UDP ports 4789 VXLAN and
+ * 2152 / 2123 GTP, GRE protocol type, MPLS bottom of stack, PPPoE data type,
+ * LLC 0x42 STP); DESIGN.md lists it. */
+enum rpkt_layer_stop {
+    RPKT_L_END = 1,        /* a terminal protocol (TCP, UDP payload, ICMP, ARP, STP, ...) */
+    RPKT_L_UNKNOWN = 2,    /* the next protocol is outside the graph: next_key holds it */
+    RPKT_L_ERR = 3,        /* the next group's parse returned Err: err_group names it */
+    RPKT_L_MAX = 4         /* RPKT_MAX_LAYERS layers walked */
+};
+#define RPKT_MAX_LAYERS 16
+
+typedef struct rpkt_layers {
+    uint8_t  n;                       /*  0 layers parsed                           */
+    uint8_t  stop;                    /*  1 rpkt_layer_stop                         */
+    uint8_t  err_group;               /*  2 RPKT_GROUP_* the walk failed in (ERR)   */
+    uint8_t  key_proto;               /*  3 UNKNOWN: protocol whose next key it is  */
+    uint16_t payload_off;             /*  4 cursor after the last layer's payload() */
+    uint16_t reserved;                /*  6                                         */
+    uint32_t payload_len;             /*  8 remaining() of that payload             */
+    uint32_t next_key;                /* 12 UNKNOWN: the unrecognised value         */
+    uint8_t  proto[RPKT_MAX_LAYERS];  /* 16 RPKT_P_* of layer k                     */
+    uint16_t off[RPKT_MAX_LAYERS];    /* 32 offset of layer k in the frame          */
+} rpkt_layers_t;
+
+#define RPKT_LAYERS_BYTES 64u
+
+/* layers_dev n * 64 B, 16-byte aligned. */
+int rpkt_gpu_layers_batch(const rpkt_batch_t* batch, rpkt_layers_t* layers_dev, void* stream);
 
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,

@@ -76,6 +76,10 @@ def lib():
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_options_batch.restype = None
+        L.oracle_layers_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_void_p]
+        L.oracle_layers_batch.restype = None
         _lib = L
     return _lib
 
@@ -191,6 +195,17 @@ def options_batch(frames, n, recs, offsets=None, stride=0, frame_len=0):
     out = np.zeros(n, dtype=OPTS_DTYPE)
     lib().oracle_options_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
                                _ptr(recs), _ptr(out))
+    return out
+
+
+def layers_batch(frames, n, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_layers_batch on the CPU: rpkt_layers_t per frame."""
+    from rpkt_amd.records import LAYERS_DTYPE
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    out = np.zeros(n, dtype=LAYERS_DTYPE)
+    lib().oracle_layers_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
+                              _ptr(out))
     return out
 
 

@@ -17,8 +17,9 @@ ARCH = os.environ.get("RPKT_OFFLOAD_ARCH", "gfx950")
 GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
 GPU_SRC = [os.path.join(HERE, "csrc", "rpkt_gpu.hip")]
+GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_proto_table.h")]     # generated, included
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
-HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h")]
+HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 
 
 def _stale(target, deps):
@@ -32,7 +33,7 @@ def source_hash():
     """Short hash of the engine sources: ties profiles/ numbers to a kernel build."""
     import hashlib
     h = hashlib.sha1()
-    for f in GPU_SRC + HDR:
+    for f in GPU_SRC + GPU_DEPS + HDR:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]
@@ -40,7 +41,7 @@ def source_hash():
 
 def build_gpu(force=False, extra=()):
     os.makedirs(OUT, exist_ok=True)
-    if force or _stale(GPU_LIB, GPU_SRC + HDR):
+    if force or _stale(GPU_LIB, GPU_SRC + GPU_DEPS + HDR):
         cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wall", '-DRPKT_SRC_HASH="%s"' % source_hash(), "-o", GPU_LIB] + \
             list(extra) + GPU_SRC

@@ -31,6 +31,7 @@
 #include <tuple>
 
 #include "../../include/rpkt_gpu.h"
+#include "rpkt_proto_table.h"
 
 namespace {
 
@@ -1683,6 +1684,297 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
 }
 
+// ---- protocol layer walk: the pktfmt-derived table interpreted per frame ----
+// kProtos / kGroups (rpkt_proto_table.h, generated by tools/pktfmt_table.py from the
+// reference's pktfmt specs) hold, per protocol, exactly what its generated parse /
+// payload / group_parse are functions of; walk_group interprets them with the
+// pktfmt codegen rules (pktfmt/src/codegen/parse.rs:138-244, payload.rs:23-87).
+// One lane per frame over a 256-B LDS window (deeper bytes from global memory).
+constexpr int kLayChunks = 16;                 // 256 B window from the 16-B phase
+constexpr int kLaySlot = 260;                  // 65 dwords: conflict-free lanes
+struct LayScratch {
+    uint8_t win[kWave * kLaySlot];             // 16 640 B
+};
+
+struct LayerWin {
+    const uint8_t* slot;                       // slot + phase: frame byte 0
+    uint32_t avail;                            // frame bytes held in LDS
+    uint32_t off;                              // frame's absolute offset
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ uint32_t at(uint32_t x) const {
+        return x < avail ? (uint32_t)slot[x] : gbyte(rs, off + x);
+    }
+    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return (at(x) << 8) | at(x + 1); }
+    // big-endian bit field (pktfmt bit order) of `bits` <= 32 at bit offset `ob` of x
+    __device__ __forceinline__ uint32_t field(uint32_t x, uint32_t ob, uint32_t bits) const {
+        const uint32_t b0 = ob >> 3, b1 = (ob + bits - 1) >> 3;
+        uint64_t v = 0;
+        for (uint32_t b = b0; b <= b1; ++b) v = (v << 8) | at(x + b);
+        const uint32_t tail = 7u - ((ob + bits - 1u) & 7u);
+        return (uint32_t)((v >> tail) & ((bits >= 32) ? 0xffffffffull : ((1ull << bits) - 1ull)));
+    }
+};
+
+__device__ __forceinline__ uint32_t len_expr(const RpktLenExpr& e, uint32_t x) {
+    switch (e.form) {                           // pktfmt UsableAlgExpr (ast/length.rs:244-283)
+        case 0: return x;
+        case 1: return x + e.a;
+        case 2: return x * e.a;
+        case 3: return (x + e.a) * e.b;
+        default: return x * e.a + e.b;
+    }
+}
+
+// group_parse + parse + payload() of group g at cursor [s, e): returns the member
+// protocol (< 0 on Err) with its header length and the trimmed packet end.
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, uint32_t g, uint32_t s, uint32_t e,
+                                          uint32_t& hl, uint32_t& end) {
+    const uint32_t r = e - s;
+    const RpktGroup G = kGroups[g];
+    if (r < G.cond_bytes) return -1;
+    int m = -1;
+    for (uint32_t k = 0; k < G.count && m < 0; ++k) {
+        const RpktProto& P = kProtos[G.first + k];
+        bool ok = true;
+        for (uint32_t c = 0; c < P.n_cond && ok; ++c) {
+            const RpktCond& C = P.cond[c];
+            const uint32_t v = Wn.field(s, C.off, C.bits);
+            bool in = false;
+            for (uint32_t q = 0; q < C.n; ++q) in |= (v >= C.lo[q] && v <= C.hi[q]);
+            ok = in;
+        }
+        if (ok) m = (int)(G.first + k);
+    }
+    if (m < 0) return -1;
+    const RpktProto& P = kProtos[m];
+    if (r < P.hdr) return -1;
+    uint32_t h = P.hdr;
+    if (P.hl_kind == 1) {
+        h = len_expr(P.hl, Wn.field(s, P.hl.off, P.hl.bits));
+    } else if (P.hl_kind == 2 || P.hl_kind == 3) {         // gre/mod.rs:68-101
+        const uint32_t ind = Wn.be16(s);
+        h = P.hl_kind == 2
+                ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
+                      ((ind & 0x1000u) ? 4u : 0u)
+                : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
+    } else if (P.hl_kind == 4) {                            // gtpv1.pktfmt header_len
+        h = (Wn.at(s) & 7u) ? 12u : 8u;
+    } else if (P.hl_kind == 5) {                            // gtpv2.pktfmt header_len
+        h = (Wn.at(s) & 8u) ? 12u : 8u;
+    }
+    if (P.hl_kind) {
+        if (P.hl_fixed >= 0) {
+            if (h != (uint32_t)P.hl_fixed) return -1;
+        } else if (h < P.hdr || h > r) {
+            return -1;
+        }
+    }
+    end = e;
+    if (P.pl_kind == 1) {                                   // payload_len
+        const uint32_t pay = len_expr(P.pl, Wn.field(s, P.pl.off, P.pl.bits));
+        if ((uint64_t)pay + h > r) return -1;
+        end = s + h + pay;
+    } else if (P.pl_kind == 2) {                            // packet_len
+        const uint32_t pkt = len_expr(P.pl, Wn.field(s, P.pl.off, P.pl.bits));
+        if (pkt < h || pkt > r) return -1;
+        end = s + pkt;
+    }
+    hl = h;
+    return m;
+}
+
+constexpr int kNextEnd = -1, kNextUnknown = -2;
+
+__device__ __forceinline__ int lay_ethertype(uint32_t et) {
+    switch (et) {
+        case 0x0800: return RPKT_G_IPV4;
+        case 0x86dd: return RPKT_G_IPV6;
+        case 0x8100: case 0x88a8: return RPKT_G_VLAN;
+        case 0x0806: return RPKT_G_ARP;
+        case 0x8847: case 0x8848: return RPKT_G_MPLS;
+        case 0x8863: case 0x8864: return RPKT_G_PPPOE;
+        default: return kNextUnknown;
+    }
+}
+__device__ __forceinline__ int lay_ipproto(uint32_t p) {
+    switch (p) {
+        case 0: return RPKT_G_IPV6_HOPBYHOP;
+        case 1: return RPKT_G_ICMPV4;
+        case 4: return RPKT_G_IPV4;
+        case 6: return RPKT_G_TCP;
+        case 17: return RPKT_G_UDP;
+        case 41: return RPKT_G_IPV6;
+        case 43: return RPKT_G_IPV6_ROUTING;
+        case 44: return RPKT_G_IPV6_FRAGMENT;
+        case 47: return RPKT_G_GRE;
+        case 51: return RPKT_G_IPV6_AUTH;
+        case 59: return kNextEnd;
+        case 60: return RPKT_G_IPV6_DESTOPTS;
+        default: return kNextUnknown;
+    }
+}
+
+// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
+// starts at h; the cursor is now [s, e).
+__device__ __forceinline__ int lay_next(const LayerWin& Wn, int p, uint32_t h, uint32_t s,
+                                        uint32_t e, uint32_t& key) {
+    switch (p) {
+        case RPKT_P_ETHER_ETHERFRAME: key = Wn.be16(h + 12); return lay_ethertype(key);
+        case RPKT_P_VLAN_VLANFRAME: key = Wn.be16(h + 2); return lay_ethertype(key);
+        case RPKT_P_ETHER_ETHERDOT3FRAME: case RPKT_P_VLAN_VLANDOT3FRAME: return RPKT_G_LLC;
+        case RPKT_P_IPV4_IPV4:
+            if (Wn.be16(h + 6) & 0x1fffu) return kNextEnd;          // non-first fragment
+            key = Wn.at(h + 9);
+            return lay_ipproto(key);
+        case RPKT_P_IPV6_IPV6: key = Wn.at(h + 6); return lay_ipproto(key);
+        case RPKT_P_IPV6_FRAGMENTHEADER:
+            if (Wn.be16(h + 2) >> 3) return kNextEnd;
+            key = Wn.at(h);
+            return lay_ipproto(key);
+        case RPKT_P_IPV6_HOPBYHOPOPTION: case RPKT_P_IPV6_DESTOPTIONS:
+        case RPKT_P_IPV6_ROUTINGHEADER: case RPKT_P_IPV6_AUTHENTICATIONHEADER:
+            key = Wn.at(h);
+            return lay_ipproto(key);
+        case RPKT_P_UDP_UDP: {
+            const uint32_t dp = Wn.be16(h + 2), sp = Wn.be16(h);
+            const uint32_t port = (dp == 4789u || dp == 2152u || dp == 2123u) ? dp
+                                : ((sp == 4789u || sp == 2152u || sp == 2123u) ? sp : 0u);
+            if (!port) return kNextEnd;
+            key = port;
+            if (port == 4789u) return RPKT_G_VXLAN;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 5;                                    // GTP version
+            return key == 1u ? RPKT_G_GTPV1 : (key == 2u ? RPKT_G_GTPV2 : kNextUnknown);
+        }
+        case RPKT_P_GRE_GRE:
+            key = Wn.be16(h + 2);
+            return key == 0x6558u ? RPKT_G_ETHER : lay_ethertype(key);
+        case RPKT_P_VXLAN_VXLAN: return RPKT_G_ETHER;
+        case RPKT_P_GTPV1_GTPV1:
+            if ((Wn.at(h) & 4u) || Wn.at(h + 1) != 255u) return kNextEnd;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 4;
+            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_MPLS_MPLS:
+            if (!(Wn.at(h + 2) & 1u)) return RPKT_G_MPLS;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 4;
+            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_PPPOE_PPPOESESSION:
+            key = Wn.be16(h + 6);
+            return key == 0x0021u ? RPKT_G_IPV4 : (key == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_LLC_LLC:
+            return (Wn.at(h) == 0x42u && Wn.at(h + 1) == 0x42u) ? RPKT_G_STP : kNextEnd;
+        default: return kNextEnd;
+    }
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
+                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                   uint32_t n, rpkt_layers_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) LayScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    LayScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    {
+        u32x4 d[kLayChunks];
+        uint32_t addr[kLayChunks];
+        uint32_t fix = 0;
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) {
+            const int c = k * kWave + lane;
+            const int q = c / kLayChunks, j = c % kLayChunks;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t ql = (uint32_t)__shfl((int)fr.len, q, kWave);
+            const uint32_t a = (qo & ~15u) + 16u * j;
+            addr[k] = (a < qo + ql) ? a : fb;
+            fix |= (uint32_t)straddles(addr[k], fb) << k;
+        }
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) {
+            const int c = k * kWave + lane;
+            u32x4 v = d[k];
+            if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kLayChunks) * kLaySlot +
+                                                              (c % kLayChunks) * 16]);
+            dst[0] = v.x;
+            dst[1] = v.y;
+            dst[2] = v.z;
+            dst[3] = v.w;
+        }
+    }
+    wave_sync();
+
+    const uint32_t ph = fr.off & 15u;
+    const LayerWin Wn{&W.win[lane * kLaySlot] + ph, (uint32_t)(kLayChunks * 16) - ph, fr.off, rs};
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    uint32_t s = 0, e = valid ? fr.len : 0u, nl = 0, stop = 0, err_g = 0, key = 0, key_p = 0;
+    int g = RPKT_G_ETHER;
+    for (;;) {
+        if (nl == RPKT_MAX_LAYERS) {
+            stop = RPKT_L_MAX;
+            break;
+        }
+        uint32_t hl = 0, end = 0;
+        const int p = walk_group(Wn, (uint32_t)g, s, e, hl, end);
+        if (p < 0) {
+            stop = RPKT_L_ERR;
+            err_g = (uint32_t)g;
+            break;
+        }
+        // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl
+        o[4 + nl / 4] |= (uint32_t)p << (8 * (nl & 3));
+        o[8 + nl / 2] |= s << (16 * (nl & 1));
+        const uint32_t h = s;
+        nl += 1;
+        e = end;
+        s += hl;
+        uint32_t k2 = 0;
+        const int nx = lay_next(Wn, p, h, s, e, k2);
+        if (nx == kNextEnd) {
+            stop = RPKT_L_END;
+            break;
+        }
+        if (nx == kNextUnknown) {
+            stop = RPKT_L_UNKNOWN;
+            key = k2;
+            key_p = (uint32_t)p;
+            break;
+        }
+        g = nx;
+    }
+    o[0] = nl | (stop << 8) | (err_g << 16) | (key_p << 24);
+    o[1] = s & 0xffffu;
+    o[2] = e - s;
+    o[3] = key;
+
+    wave_sync();
+    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* dst = reinterpret_cast<u32x4*>(out + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &dst[c]);
+    }
+}
+
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
 // chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
 template <int U, bool NT>
@@ -2065,6 +2357,21 @@ int rpkt_gpu_options_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
     return launch(options_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
                   recs_dev, opts_dev);
+}
+
+int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void* stream) {
+    if (!b || !layers_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)layers_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(layers_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  layers_dev);
 }
 
 // Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from .build import GPU_LIB
-from .records import OPTS_BYTES, REC_BYTES, F_FLOW_EV
+from .records import LAYERS_BYTES, OPTS_BYTES, REC_BYTES, F_FLOW_EV
 
 RPKT_OK = 0
 ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN"}
@@ -48,7 +48,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
-           "rpkt_gpu_options_batch"]
+           "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch"]
 
 _lib = None
 
@@ -103,6 +103,9 @@ def lib():
         L.rpkt_gpu_options_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_options_batch.restype = ctypes.c_int
+        L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        L.rpkt_gpu_layers_batch.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -329,3 +332,15 @@ def options_batch(batch, recs, opts=None, stream=None):
                                       _stream_ptr(stream))
     _check(rc, "rpkt_gpu_options_batch")
     return opts
+
+
+def layers_batch(batch, out=None, stream=None):
+    """rpkt_gpu_layers_batch: the protocol stack of every frame (pktfmt-derived
+    walk); returns the uint8 tensor of n * 64-byte rpkt_layers_t."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(batch.n * LAYERS_BYTES, dtype=torch.uint8, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_layers_batch(ctypes.byref(d), out.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_layers_batch")
+    return out

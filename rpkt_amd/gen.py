@@ -12,6 +12,8 @@ Config ids follow BASELINE.json `configs` (1-based like SURVEY.md §8d):
     examples/jumboframe_tx.rs:45; mempool_alloc(.., 2048 + 128, ..) in tests/pbuf.rs)
   8 chain fuzz: config-6 style frames up to 9000 B cut into 1..6 segments at random
     and header-boundary positions (empty segments included), odd slot alignments
+  9 protocol mix for the layer walk: 1,048,576 frames drawn from the reference's
+    captures, a third cut short and a third with random header bytes (make_mix)
 """
 import ctypes
 import os
@@ -21,8 +23,8 @@ import numpy as np
 from .build import GEN_LIB, build_gen
 
 DEFAULT_N = {1: 1000, 2: 1 << 20, 3: 1 << 20, 4: 8 << 20, 5: 4 << 20, 6: 1 << 16,
-             7: 1 << 18, 8: 1 << 15}
-DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8}
+             7: 1 << 18, 8: 1 << 15, 9: 1 << 20}
+DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9}
 STRIDED = {1: 64, 2: 64, 3: 1500}
 CHAINED = (7, 8)
 FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3}   # config 2 = extract + IPv4 header sum
@@ -189,3 +191,50 @@ def make_chains(config, n=None, seed=None, threads=None, layout=None):
     segs = np.stack([dst_off.astype(np.uint32), sl32], axis=1)
     return HostChains(config, n, seed, buf, np.ascontiguousarray(segs),
                       chain_first.astype(np.uint32), lens.astype(np.uint32))
+
+
+def fixture_frames(root=None):
+    """The reference's captures (tests/golden/packets/*.dat), sorted by name."""
+    d = root or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "tests", "golden", "packets")
+    out = []
+    for fn in sorted(os.listdir(d)):
+        with open(os.path.join(d, fn)) as fh:
+            s = fh.read().strip()
+        out.append(bytes(int(s[i:i + 2], 16) for i in range(0, len(s), 2)))
+    return out
+
+
+def make_mix(n=1 << 20, seed=9, fuzz=True):
+    """Config 9 (the protocol-walk workload): frames drawn from the reference's 53
+    captures (ARP, 802.3/LLC/STP, QinQ, MPLS, PPPoE, GRE v0/v1, VXLAN, GTPv1/v2,
+    IPv6 extension headers, IPv4 options, TCP, UDP), packed.  With `fuzz`, a third
+    of them are cut at a random length and a third get 1-3 random header bytes."""
+    base = fixture_frames()
+    rng = np.random.default_rng(seed)
+    pick = rng.integers(0, len(base), n)
+    lens = np.array([len(b) for b in base], dtype=np.int64)[pick]
+    mode = rng.integers(0, 3, n) if fuzz else np.zeros(n, dtype=np.int64)
+    cut = np.where(mode == 1, (rng.random(n) * (lens + 1)).astype(np.int64), lens)
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(cut, out=offsets[1:])
+    frames = np.zeros(int(offsets[-1]) + 16, dtype=np.uint8)
+    pool = [np.frombuffer(b, dtype=np.uint8) for b in base]
+    order = np.argsort(pick, kind="stable")
+    for k in range(len(base)):                        # vectorised copy per capture
+        idx = order[np.searchsorted(pick[order], k):np.searchsorted(pick[order], k + 1)]
+        if not idx.size:
+            continue
+        L = len(pool[k])
+        rows = np.minimum(cut[idx], L)
+        tgt = offsets[idx][:, None] + np.arange(L)[None, :]
+        mask = np.arange(L)[None, :] < rows[:, None]
+        frames[tgt[mask]] = np.broadcast_to(pool[k], (idx.size, L))[mask]
+    flip = np.nonzero(mode == 2)[0]
+    nb = rng.integers(1, 4, flip.size)
+    for j in range(3):
+        sel = flip[nb > j]
+        pos = offsets[sel] + (rng.random(sel.size) * np.minimum(cut[sel], 80)).astype(np.int64)
+        ok = cut[sel] > 0
+        frames[pos[ok]] = rng.integers(0, 256, ok.sum(), dtype=np.uint8)
+    return HostBatch(9, n, seed, frames[:int(offsets[-1])], offsets.astype(np.uint32), 0, 0)

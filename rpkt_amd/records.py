@@ -53,6 +53,28 @@ IP_KINDS = ("Eol", "Nop", "Timestamp", "RecordRoute", "RouteAlert", "CommercialS
             "StrictSourceRoute", "LooseSourceRoute")
 
 
+LAYERS_BYTES = 64
+LAYERS_DTYPE = np.dtype([        # rpkt_layers_t (include/rpkt_gpu.h), 64 B
+    ("n", "u1"), ("stop", "u1"), ("err_group", "u1"), ("key_proto", "u1"),
+    ("payload_off", "<u2"), ("reserved", "<u2"), ("payload_len", "<u4"), ("next_key", "<u4"),
+    ("proto", "u1", (16,)), ("off", "<u2", (16,)),
+])
+assert LAYERS_DTYPE.itemsize == LAYERS_BYTES
+LAYER_STOP = {"END": 1, "UNKNOWN": 2, "ERR": 3, "MAX": 4}
+
+
+def protocol_names():
+    """Protocol id -> name, from include/rpkt_protocols.h."""
+    import os
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                       "rpkt_protocols.h")
+    out = {}
+    for m in re.finditer(r"#define RPKT_P_(\w+) (\d+)", open(hdr).read()):
+        out[int(m.group(2))] = m.group(1)
+    return out
+
+
 def trace_kinds(trace, count, names):
     """The first min(count, 16) option kinds of a *_trace field, by name."""
     return [names[((int(trace) >> (4 * k)) & 15) - 1] for k in range(min(int(count), 16))]
