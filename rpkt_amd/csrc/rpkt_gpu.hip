@@ -1706,12 +1706,11 @@ struct LayerWin {
     }
     __device__ __forceinline__ uint32_t be16(uint32_t x) const { return (at(x) << 8) | at(x + 1); }
     // big-endian bit field (pktfmt bit order) of `bits` <= 32 at bit offset `ob` of x
+    // (cond and length fields are at most 16 bits wide: 4 bytes always cover them)
     __device__ __forceinline__ uint32_t field(uint32_t x, uint32_t ob, uint32_t bits) const {
-        const uint32_t b0 = ob >> 3, b1 = (ob + bits - 1) >> 3;
-        uint64_t v = 0;
-        for (uint32_t b = b0; b <= b1; ++b) v = (v << 8) | at(x + b);
-        const uint32_t tail = 7u - ((ob + bits - 1u) & 7u);
-        return (uint32_t)((v >> tail) & ((bits >= 32) ? 0xffffffffull : ((1ull << bits) - 1ull)));
+        const uint32_t a = x + (ob >> 3);
+        const uint32_t v = (at(a) << 24) | (at(a + 1) << 16) | (at(a + 2) << 8) | at(a + 3);
+        return (v << (ob & 7u)) >> (32u - bits);
     }
 };
 
@@ -1727,14 +1726,15 @@ __device__ __forceinline__ uint32_t len_expr(const RpktLenExpr& e, uint32_t x) {
 
 // group_parse + parse + payload() of group g at cursor [s, e): returns the member
 // protocol (< 0 on Err) with its header length and the trimmed packet end.
-__device__ __forceinline__ int walk_group(const LayerWin& Wn, uint32_t g, uint32_t s, uint32_t e,
-                                          uint32_t& hl, uint32_t& end) {
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, const RpktProto* __restrict__ protos,
+                                          const RpktGroup* __restrict__ groups, uint32_t g,
+                                          uint32_t s, uint32_t e, uint32_t& hl, uint32_t& end) {
     const uint32_t r = e - s;
-    const RpktGroup G = kGroups[g];
+    const RpktGroup G = groups[g];
     if (r < G.cond_bytes) return -1;
     int m = -1;
     for (uint32_t k = 0; k < G.count && m < 0; ++k) {
-        const RpktProto& P = kProtos[G.first + k];
+        const RpktProto& P = protos[G.first + k];
         bool ok = true;
         for (uint32_t c = 0; c < P.n_cond && ok; ++c) {
             const RpktCond& C = P.cond[c];
@@ -1746,7 +1746,7 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, uint32_t g, uint32
         if (ok) m = (int)(G.first + k);
     }
     if (m < 0) return -1;
-    const RpktProto& P = kProtos[m];
+    const RpktProto& P = protos[m];
     if (r < P.hdr) return -1;
     uint32_t h = P.hdr;
     if (P.hl_kind == 1) {
@@ -1874,6 +1874,18 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                    uint32_t n, rpkt_layers_t* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) LayScratch scratch[kWavesPerBlock];
+    // the protocol table in LDS: lanes walk different protocols, so table reads are
+    // per-lane (divergent) loads; from LDS they cost tens of cycles instead of a
+    // global-memory round trip per dependent lookup
+    __shared__ __attribute__((aligned(16))) RpktProto protos[RPKT_N_PROTOS];
+    __shared__ __attribute__((aligned(16))) RpktGroup groups[RPKT_N_GROUPS];
+    {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(kProtos);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(protos);
+        for (uint32_t k = threadIdx.x; k < sizeof(kProtos) / 4; k += blockDim.x) dst[k] = src[k];
+        if (threadIdx.x < RPKT_N_GROUPS) groups[threadIdx.x] = kGroups[threadIdx.x];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     LayScratch& W = scratch[wid];
@@ -1928,7 +1940,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             break;
         }
         uint32_t hl = 0, end = 0;
-        const int p = walk_group(Wn, (uint32_t)g, s, e, hl, end);
+        const int p = walk_group(Wn, protos, groups, (uint32_t)g, s, e, hl, end);
         if (p < 0) {
             stop = RPKT_L_ERR;
             err_g = (uint32_t)g;

@@ -285,6 +285,9 @@ def main(ref="/root/reference"):
     t = build(ref)
     for g in t["groups"]:                      # members must be consecutive ids
         assert g["members"] == list(range(g["members"][0], g["members"][0] + len(g["members"])))
+    for p in t["packets"]:                     # the kernel reads fields through 4 bytes
+        for f in [c for c in p["cond"]] + [e for e in (p["hl"], p["pl"]) if e]:
+            assert f["off"] % 8 + f["bits"] <= 32, (p["name"], f)
     with open(os.path.join(ROOT, "rpkt_amd", "csrc", "rpkt_proto_table.h"), "w") as fh:
         fh.write(c_header(t))
     with open(os.path.join(ROOT, "include", "rpkt_protocols.h"), "w") as fh:
