@@ -107,3 +107,21 @@ def test_engine_refuses_cpu_fallback():
 def test_cpp_example_builds_against_header():
     from rpkt_amd.build import build_example
     assert os.path.exists(build_example())
+
+
+def test_layers_layout_matches_header():
+    src = open(HDR).read()
+    body = src[src.index("typedef struct rpkt_layers {"):]
+    body = body[:body.index("}")]
+    offs = [int(m) for m in re.findall(r";\s*/\*\s*(\d+) ", body)]
+    assert offs == [records.LAYERS_DTYPE.fields[n][1] for n in records.LAYERS_DTYPE.names]
+
+
+def test_protocol_ids_match_table():
+    import json
+    t = json.load(open(os.path.join(os.path.dirname(HDR), "..", "tests", "golden",
+                                    "proto_table.json")))
+    names = records.protocol_names()
+    assert len(names) == len(t["packets"])
+    for p in t["packets"]:
+        assert names[p["id"]] == ("%s_%s" % (p["spec"], p["name"])).upper()
