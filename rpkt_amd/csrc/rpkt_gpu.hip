@@ -171,72 +171,71 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
 
 // Flattened chunk stream over the tile: lane q owns absolute byte range
 // [s_abs, e_abs) (empty allowed); returns that range's absolute-phase word sum.
-// Consecutive lanes read consecutive 16-byte chunks of the concatenated ranges
-// (coalesced whatever the frame sizes).  Each chunk's word sum enters a wave-wide
-// inclusive scan; a range's sum is the scan value at its last chunk minus the value
-// before its first.  Loads are double-buffered: batch k+1 is in flight while batch k
-// is summed, and every batch issues unconditionally (lanes past the end read the
-// descriptor's out-of-range offset: zeros, no traffic) so the vmcnt waits stay exact.
-// `oob` is the descriptor's byte range.
+// The range splits into full 16-byte chunks [ceil16(s), floor16(e)) and at most two
+// partial edge chunks.  The full chunks of all 64 ranges are concatenated and read
+// by consecutive lanes (coalesced whatever the frame sizes); each chunk's plain word
+// sum enters a wave-wide inclusive scan, and a range's sum is the scan value at its
+// last chunk minus the value before its first.  The edge chunks are loaded by their
+// owner lane alongside the stream and summed under a byte mask once per range, so
+// the per-chunk path carries no masking, no clipping and no conditional load.  Loads
+// are double-buffered (batch k+1 in flight while batch k is summed) and every load
+// issues unconditionally (lanes past the end read the descriptor's out-of-range
+// offset: zeros, no traffic), so the vmcnt waits stay exact.  A full chunk ends at or
+// before its range end, so it never straddles the end of the buffer; only an edge
+// chunk can, and it is re-read exactly after the loop.  `oob` = the descriptor's range.
 struct StreamBatch {
     u32x4 d[kStreamUnroll];
-    uint32_t a[kStreamUnroll];       // chunk address
-    uint32_t m[kStreamUnroll];       // owner q | lo << 8 | hi << 13 | first << 18 | last << 19 |
-                                     // valid << 20 (lo, hi clipped to 0..16, chunk-relative)
+    uint32_t m[kStreamUnroll];       // owner q | first << 8 | last << 9
 };
 
-// Resolve chunk c = base + u*64 + lane of the concatenated ranges: owner lane (the
-// ranges are in chunk order, so a lane's cursor only moves forward; binary search
-// only for jumps), address, and the clip/first/last metadata, so that consuming
-// the chunk needs no further LDS reads.
+// Per-lane cursor over the concatenated full chunks: the owner range q of the lane's
+// current chunk, its chunk span [p0, p1), and off = ceil16(s_q) - 16 * p0, so chunk c
+// of range q is at off + 16 c.  The ranges are in chunk order, so a cursor only moves
+// forward: one step to the next range, binary search only for jumps.
+struct StreamCursor { uint32_t q, p0, p1, off; };
+
+__device__ __forceinline__ void cursor_load(const WaveScratch& W, StreamCursor& k, uint32_t q) {
+    k.q = q;
+    k.p0 = W.pref[q];
+    k.p1 = W.pref[q + 1];
+    k.off = W.s[q];
+}
+
 template <int AUX>
 __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
                                              const WaveScratch& W, uint32_t total, uint32_t base,
-                                             int lane, uint32_t& cur, StreamBatch& B) {
+                                             int lane, StreamCursor& k, StreamBatch& B) {
 #pragma unroll
     for (int u = 0; u < kStreamUnroll; ++u) {
         const uint32_t c = base + u * kWave + lane;
         const bool valid = c < total;
-        uint32_t p1 = W.pref[cur + 1];
-        if (valid && p1 <= c) {
-            if (W.pref[cur + 2] > c) {
-                cur += 1;
-            } else {
-                uint32_t lo = 0;
+        if (valid && k.p1 <= c) {
+            uint32_t q = k.q + 1;
+            if (W.pref[q + 1] <= c) {
+                q = 0;
 #pragma unroll
                 for (int step = 32; step; step >>= 1)
-                    if (W.pref[lo + step] <= c) lo += step;
-                cur = lo;
+                    if (W.pref[q + step] <= c) q += step;
             }
-            p1 = W.pref[cur + 1];
+            cursor_load(W, k, q);
         }
-        const uint32_t q = cur, p0 = W.pref[q], sq = W.s[q], eq = W.e[q];
-        const uint32_t a = (sq & ~15u) + 16u * (c - p0);
-        const int lo = (int)sq - (int)a, hi = (int)eq - (int)a;
-        const uint32_t lo_c = lo < 0 ? 0u : (uint32_t)lo;                 // 0..15
-        const uint32_t hi_c = hi > 16 ? 16u : (hi < 0 ? 0u : (uint32_t)hi);
-        B.a[u] = a;
-        B.m[u] = q | (lo_c << 8) | (hi_c << 13) | ((uint32_t)(c == p0) << 18) |
-                 ((uint32_t)(c + 1 == p1) << 19) | ((uint32_t)valid << 20);
-        B.d[u] = load16_fast<AUX>(rs, valid ? a : oob);
+        // lanes past the end never match first/last: c >= total >= p1 > p0
+        B.m[u] = k.q | ((uint32_t)(c == k.p0) << 8) | ((uint32_t)(c + 1 == k.p1) << 9);
+        B.d[u] = load16_fast<AUX>(rs, valid ? k.off + 16u * c : oob);
     }
 }
 
-__device__ __forceinline__ void stream_consume(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
-                                               WaveScratch& W, int lane, uint32_t& run,
+__device__ __forceinline__ void stream_consume(WaveScratch& W, uint32_t& run,
                                                const StreamBatch& B) {
 #pragma unroll
     for (int u = 0; u < kStreamUnroll; ++u) {
-        const uint32_t m = B.m[u];
-        const int lo = (int)((m >> 8) & 31u), hi = (int)((m >> 13) & 31u);
-        uint32_t v = chunk_sum(B.d[u], lo, hi);                 // invalid lanes: d = 0
-        if (__builtin_expect((m >> 20) && straddles(B.a[u], oob), 0))   // buffer's last chunk
-            v = chunk_sum(load16(rs, B.a[u], oob), lo, hi);
+        const u32x4 d = B.d[u];
+        const uint32_t v = hsum(d.w, hsum(d.z, hsum(d.y, hsum(d.x, 0u))));
         const uint32_t sc = wave_incl_scan(v) + run;
         run = __builtin_amdgcn_readlane(sc, 63);
-        const uint32_t q = m & 63u;
-        if (m & (1u << 18)) W.first[q] = sc - v;
-        if (m & (1u << 19)) W.last[q] = sc;
+        const uint32_t m = B.m[u], q = m & 63u;
+        if (m & (1u << 8)) W.first[q] = sc - v;
+        if (m & (1u << 9)) W.last[q] = sc;
     }
 }
 
@@ -244,34 +243,67 @@ template <int AUX = 0>
 __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
                                                     uint32_t s_abs, uint32_t e_abs,
                                                     WaveScratch& W, int lane) {
-    const uint32_t nch = e_abs > s_abs ? ((e_abs - 1) >> 4) - (s_abs >> 4) + 1 : 0;
+    const bool ne = e_abs > s_abs;
+    const uint32_t S = (s_abs + 15u) & ~15u, E = e_abs & ~15u;
+    // edge chunks: head [s, min(e, S)) in the chunk at floor16(s); tail [max(s, E), e)
+    // in the chunk at E when that is not the head chunk
+    const uint32_t hs = s_abs & ~15u;
+    const bool head = ne && (s_abs & 15u);
+    const bool tail = ne && (e_abs & 15u) && E >= S;
+    const uint32_t ha = head ? hs : oob, ta = tail ? E : oob;
+    const u32x4 hd = load16_fast<AUX>(rs, ha);
+    const u32x4 td = load16_fast<AUX>(rs, ta);
+
+    // the edge sums are taken once the first stream batch is in flight, so no edge load
+    // is still outstanding when the loop starts (its vmcnt waits then count exactly the
+    // stream's own loads)
+    auto edges = [&]() -> uint32_t {
+        u32x4 h = hd, t = td;
+        // a chunk straddling the buffer end was dropped whole by the range check: re-read
+        // it as the last 16 in-range bytes (rare path)
+        const bool hfix = head && straddles(hs, oob), tfix = tail && straddles(E, oob);
+        if (__builtin_expect(__ballot(hfix || tfix) != 0, 0)) {
+            if (hfix) h = load16(rs, hs, oob);
+            if (tfix) t = load16(rs, E, oob);
+        }
+        uint32_t x = 0;
+        if (head) {
+            const uint32_t he = e_abs - hs;
+            x = chunk_sum(h, (int)(s_abs - hs), he < 16u ? (int)he : 16);
+        }
+        if (tail) x += chunk_sum(t, 0, (int)(e_abs - E));
+        return x;
+    };
+
+    const uint32_t nch = ne && E > S ? (E - S) >> 4 : 0;
     const uint32_t incl = wave_incl_scan(nch);
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    if (total == 0) return 0;                                    // wave-uniform
+    if (total == 0) return edges();                              // wave-uniform
     W.pref[lane] = incl - nch;
     if (lane == 63) W.pref[64] = incl;
-    W.s[lane] = s_abs;
-    W.e[lane] = e_abs;
+    W.s[lane] = S - 16u * (incl - nch);
     W.first[lane] = 0;
     W.last[lane] = 0;
     wave_sync();
 
     constexpr uint32_t kBatch = kWave * kStreamUnroll;
-    uint32_t run = 0, cur = 0;
+    uint32_t run = 0;
+    StreamCursor k;
+    cursor_load(W, k, 0);
     StreamBatch A, B;
     uint32_t base = 0;
-    stream_issue<AUX>(rs, oob, W, total, base, lane, cur, A);
+    stream_issue<AUX>(rs, oob, W, total, base, lane, k, A);
+    const uint32_t edge = edges();
     for (;;) {
-        stream_issue<AUX>(rs, oob, W, total, base + kBatch, lane, cur, B);
-        stream_consume(rs, oob, W, lane, run, A);
-        if (base + kBatch >= total) break;
-        stream_issue<AUX>(rs, oob, W, total, base + 2 * kBatch, lane, cur, A);
-        stream_consume(rs, oob, W, lane, run, B);
-        if (base + 2 * kBatch >= total) break;
+        stream_issue<AUX>(rs, oob, W, total, base + kBatch, lane, k, B);
+        stream_consume(W, run, A);
+        stream_issue<AUX>(rs, oob, W, total, base + 2 * kBatch, lane, k, A);
+        stream_consume(W, run, B);
         base += 2 * kBatch;
+        if (base >= total) break;
     }
     wave_sync();
-    return nch ? W.last[lane] - W.first[lane] : 0;
+    return (nch ? W.last[lane] - W.first[lane] : 0) + edge;
 }
 
 struct Frame { uint32_t off, len; };
