@@ -2062,6 +2062,36 @@ void read_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, uint32_t* __re
     if (r == 0x12345678u) out[t] = r;       // keeps the loads live, never taken in practice
 }
 
+// Same-traffic reference for the parse: each wave reads its 64-frame tile's bytes as
+// one contiguous non-temporal 16-B/lane stream and writes 64 records (80 B each) with
+// non-temporal stores, like parse_kernel, but does no parse work.  `tile_bytes` is the
+// tile's span (64 x stride); the last tile is clipped.
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                        uint32_t tile_bytes, uint32_t n, u32x4* __restrict__ out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t t = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const uint32_t p0 = t * kWave;
+    if (p0 >= n) return;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+    const uint32_t s = t * tile_bytes;
+    const uint32_t e = s + tile_bytes < frames_bytes ? s + tile_bytes : frames_bytes;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (uint32_t a = (s & ~15u) + 16u * lane; a < e; a += 16u * kWave * 8) {
+        u32x4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = load16_fast<2>(rs, a + 16u * kWave * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u];
+    }
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane;
+        if (c / 5 < nrec) __builtin_nontemporal_store(acc + c, &out[(size_t)p0 * 5 + c]);
+    }
+}
+
 // ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
 // One workgroup per CU-sized slice of the events; each keeps {pkts, bytes,
 // ip_bad | l4_bad << 16} per bucket in LDS (u32; a slice holds < 65536 events,
@@ -2454,6 +2484,10 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
             return launch(read_ref_kernel, dim3(4096), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
                           (uint32_t*)recs);
+        case 15:
+            if (b->offsets_dev || b->n == 0) return RPKT_E_INVAL;
+            return launch(tile_rw_ref_kernel, dim3(grid), dim3(per_block), 0, st, b->frames_dev,
+                          (uint32_t)b->frames_bytes, b->stride * kWave, b->n, (u32x4*)recs);
         case 13:
             return launch(copy_ref_kernel<8, false>, dim3(8192), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),

@@ -2,7 +2,9 @@
 
 Times, interleaved in one process (cdna_hip_programming.md §5.4 rule 24):
   v0 product kernel, v1 window only (no parse), v2 no L4 stream, v3 no record
-  stores, v10 streaming-copy reference (same read + write bytes, coalesced).
+  stores, v10 streaming-copy reference (same read + write bytes, coalesced), v14 grid-stride
+  read-only reference, v15 same-traffic tile reference (strided configs: each wave streams
+  its tile's bytes with nt loads and writes 64 records, no parse).
 Usage: python tools/ablate.py [--configs 2,3] [--rounds 5] [--launches 20]
 """
 import argparse
