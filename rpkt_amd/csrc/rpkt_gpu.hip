@@ -1721,27 +1721,39 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 // reference's pktfmt specs) hold, per protocol, exactly what its generated parse /
 // payload / group_parse are functions of; walk_group interprets them with the
 // pktfmt codegen rules (pktfmt/src/codegen/parse.rs:138-244, payload.rs:23-87).
-// One lane per frame over a 256-B LDS window (deeper bytes from global memory).
-constexpr int kLayChunks = 16;                 // 256 B window from the 16-B phase
-constexpr int kLaySlot = 260;                  // 65 dwords: conflict-free lanes
+// One lane per frame over a 128-B LDS window (deeper bytes, about 1 % of the walks of
+// the capture mix, from global memory).  128 B keeps the block at 37 KB of LDS, so four
+// blocks (16 waves) fit a CU: the walk is a chain of dependent LDS round trips, and
+// occupancy is what hides them.
+constexpr int kLayChunks = 8;                  // 128 B window from the 16-B phase
+constexpr int kLaySlot = 132;                  // 33 dwords: conflict-free lanes
 struct LayScratch {
-    uint8_t win[kWave * kLaySlot];             // 16 640 B
+    uint8_t win[kWave * kLaySlot];             // 8448 B
 };
 
 struct LayerWin {
-    const uint8_t* slot;                       // slot + phase: frame byte 0
+    const uint8_t* base;                       // the lane's slot; frame byte x at ph + x
+    uint32_t ph;                               // frame offset & 15
     uint32_t avail;                            // frame bytes held in LDS
     uint32_t off;                              // frame's absolute offset
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ uint32_t at(uint32_t x) const {
-        return x < avail ? (uint32_t)slot[x] : gbyte(rs, off + x);
+        return x < avail ? (uint32_t)base[ph + x] : gbyte(rs, off + x);
     }
-    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return (at(x) << 8) | at(x + 1); }
+    // frame bytes x..x+3 as a little-endian dword: two aligned LDS dwords and a byte
+    // align when all four are in the window, else byte by byte
+    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
+        if (x + 4u <= avail) {
+            const uint32_t y = ph + x, a = y & ~3u;
+            return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
+        }
+        return at(x) | (at(x + 1) << 8) | (at(x + 2) << 16) | (at(x + 3) << 24);
+    }
+    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
     // big-endian bit field (pktfmt bit order) of `bits` <= 32 at bit offset `ob` of x
     // (cond and length fields are at most 16 bits wide: 4 bytes always cover them)
     __device__ __forceinline__ uint32_t field(uint32_t x, uint32_t ob, uint32_t bits) const {
-        const uint32_t a = x + (ob >> 3);
-        const uint32_t v = (at(a) << 24) | (at(a + 1) << 16) | (at(a + 2) << 8) | at(a + 3);
+        const uint32_t v = bswap32(dw(x + (ob >> 3)));
         return (v << (ob & 7u)) >> (32u - bits);
     }
 };
@@ -1960,7 +1972,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     wave_sync();
 
     const uint32_t ph = fr.off & 15u;
-    const LayerWin Wn{&W.win[lane * kLaySlot] + ph, (uint32_t)(kLayChunks * 16) - ph, fr.off, rs};
+    const LayerWin Wn{&W.win[lane * kLaySlot], ph, (uint32_t)(kLayChunks * 16) - ph, fr.off, rs};
     uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0;

@@ -220,7 +220,7 @@ def c_header(t):
          "// (pktfmt/protocols/*.pktfmt); do not edit.  See that script for the meaning.",
          "#pragma once", "#include <stdint.h>", "",
          "struct RpktLenExpr { uint16_t off; uint8_t bits; uint8_t form; uint16_t a, b; };",
-         "struct RpktCond { uint16_t off; uint8_t bits; uint8_t n; uint32_t lo[3], hi[3]; };",
+         "struct RpktCond { uint16_t off; uint8_t bits; uint8_t n; uint16_t lo[3], hi[3]; };",
          "struct RpktProto {",
          "    uint16_t hdr;          // fixed header bytes",
          "    uint8_t hl_kind;       // 0 none, 1 expr, 2 gre, 3 gre_pptp, 4 gtpv1, 5 gtpv2",
@@ -288,6 +288,8 @@ def main(ref="/root/reference"):
     for p in t["packets"]:                     # the kernel reads fields through 4 bytes
         for f in [c for c in p["cond"]] + [e for e in (p["hl"], p["pl"]) if e]:
             assert f["off"] % 8 + f["bits"] <= 32, (p["name"], f)
+        for c in p["cond"]:                    # condition fields and ranges are 16-bit
+            assert c["bits"] <= 16 and all(0 <= v < 1 << 16 for r in c["ranges"] for v in r)
     with open(os.path.join(ROOT, "rpkt_amd", "csrc", "rpkt_proto_table.h"), "w") as fh:
         fh.write(c_header(t))
     with open(os.path.join(ROOT, "include", "rpkt_protocols.h"), "w") as fh:

@@ -107,6 +107,55 @@ __global__ __launch_bounds__(256) void seg_rw(const uint8_t* in, uint32_t bytes,
     }
 }
 
+// E: read stream + records, the records of all 4 waves of a block written together at
+// the end of the block (20 KB contiguous per block) after a barrier
+__global__ __launch_bounds__(256) void seg_rw_block(const uint8_t* in, uint32_t bytes, uint32_t seg,
+                                                    u32x4* rec, uint32_t rec_per_seg) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t s = w * seg;
+    const uint32_t e = s + seg < bytes ? s + seg : bytes;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)bytes, 0x00020000);
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t a = s + lane * 16; a < e; a += 1024 * 8) {
+        u32x4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = ld(r, a + u * 1024, 2);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u];
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < 4 * rec_per_seg; k += 256)
+        __builtin_nontemporal_store(acc + k, &rec[(size_t)blockIdx.x * 4 * rec_per_seg + k]);
+}
+// F: pure write stream
+__global__ __launch_bounds__(256) void wr_only(u32x4* out, uint32_t n16) {
+    const uint32_t T = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += T)
+        __builtin_nontemporal_store(u32x4{i, i, i, i}, &out[i]);
+}
+// G: records written at the START of each wave's segment (then the read)
+__global__ __launch_bounds__(256) void seg_wr_first(const uint8_t* in, uint32_t bytes, uint32_t seg,
+                                                    u32x4* rec, uint32_t rec_per_seg, uint32_t* o) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t s = w * seg;
+    if (s >= bytes) return;
+    const uint32_t e = s + seg < bytes ? s + seg : bytes;
+    for (uint32_t k = lane; k < rec_per_seg; k += 64)
+        __builtin_nontemporal_store(u32x4{k, w, 0, 0}, &rec[(size_t)w * rec_per_seg + k]);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)bytes, 0x00020000);
+    u32x4 acc = {0, 0, 0, 0};
+    for (uint32_t a = s + lane * 16; a < e; a += 1024 * 8) {
+        u32x4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = ld(r, a + u * 1024, 2);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u];
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) o[threadIdx.x] = 1;
+}
+
 template <typename F>
 static float timeit(F f, int reps) {
     hipEvent_t a, b;
@@ -188,6 +237,12 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((seg_rw<8, 2>), dim3((nw + 3) / 4), dim3(256), 0, 0, buf, bytes, 96000u, rec, 320u); }, reps));
         rep("seg_rw 96000 U8 nt + 5120 B recs aux3", timeit([&] {
             hipLaunchKernelGGL((seg_rw<8, 3>), dim3((nw + 3) / 4), dim3(256), 0, 0, buf, bytes, 96000u, rec, 320u); }, reps));
+        rep("seg_rw_block 96000 nt + 20 KB recs/block", timeit([&] {
+            hipLaunchKernelGGL(seg_rw_block, dim3((nw + 3) / 4), dim3(256), 0, 0, buf, bytes, 96000u, rec, 320u); }, reps));
+        rep("seg_wr_first 96000 nt, recs first", timeit([&] {
+            hipLaunchKernelGGL(seg_wr_first, dim3((nw + 3) / 4), dim3(256), 0, 0, buf, bytes, 96000u, rec, 320u, out); }, reps));
+        float ms = timeit([&] { hipLaunchKernelGGL(wr_only, dim3(8192), dim3(256), 0, 0, rec, 1048576u * 5u); }, reps);
+        printf("%-44s %8.1f us  %6.3f TB/s (of 84 MB)\n", "wr_only 84 MB nt", ms * 1e3, 83886080.0 / (ms * 1e-3) / 1e12);
         rep("seg_rw 96000 U8 nt + 0 recs", timeit([&] {
             hipLaunchKernelGGL((seg_rw<8, 1>), dim3((nw + 3) / 4), dim3(256), 0, 0, buf, bytes, 96000u, rec, 0u); }, reps));
     }
