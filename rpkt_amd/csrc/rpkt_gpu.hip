@@ -1493,18 +1493,33 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
 // record read and the 64-B output only).  Lane-per-frame walk over LDS bytes with
 // the per-type parse rules of the generated option views (oracle/rpkt_oracle_opts.c
 // cites them); results staged through LDS and stored as 4 KiB of coalesced rows.
-constexpr int kOptChunks = 10;                 // 160 B from the frame's 16-B phase:
-constexpr int kOptSlot = 164;                  // covers l4 + doff*4 <= 142 at any phase
+constexpr int kOptChunks = 8;                  // 128 B from the 16-B phase of the first
+constexpr int kOptSlot = 132;                  // option byte: both slices span at most
+                                               // ihl4 + 40 <= 100 B, + 15 of phase
 struct OptScratch {
-    uint8_t win[kWave * kOptSlot];             // 10 496 B (stride 41 dwords: conflict-free)
-};
+    uint8_t win[kWave * kOptSlot];             // 8448 B (stride 33 dwords: conflict-free),
+};                                             // so four blocks (16 waves) fit a CU
 static_assert(kWave * 21 * 4 <= kWave * kOptSlot, "record stage fits the option window");
 
-__device__ __forceinline__ uint32_t lds8(const uint8_t* p, uint32_t a) { return p[a]; }
+// Option bytes in LDS: frame byte x of this lane at base[x + bias] (bias = the window's
+// phase minus the first option byte's frame offset; only x >= that offset is read).
+struct OptWin {
+    const uint8_t* base;                       // the lane's slot (4-aligned)
+    uint32_t bias;
+    __device__ __forceinline__ uint32_t b(uint32_t x) const { return base[x + bias]; }
+    // frame bytes x..x+3, little-endian: two aligned LDS dwords and a byte align
+    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
+        const uint32_t y = x + bias, a = y & ~3u;
+        return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
+    }
+    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
+    __device__ __forceinline__ uint32_t be32(uint32_t x) const { return bswap32(dw(x)); }
+};
 
-// returns option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown
-__device__ __forceinline__ int tcp_opt_len(const uint8_t* s, uint32_t at, uint32_t n, int& kind) {
-    const uint32_t t = lds8(s, at), hl = n >= 2 ? lds8(s, at + 1) : 0u;
+// returns option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown;
+// d0 = the option's first four bytes (type, length, ...)
+__device__ __forceinline__ int tcp_opt_len(uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
     switch (t) {
         case 0: kind = 0; return 1;
         case 1: kind = 1; return 1;
@@ -1517,8 +1532,8 @@ __device__ __forceinline__ int tcp_opt_len(const uint8_t* s, uint32_t at, uint32
         default: return -1;
     }
 }
-__device__ __forceinline__ int ip_opt_len(const uint8_t* s, uint32_t at, uint32_t n, int& kind) {
-    const uint32_t t = lds8(s, at), hl = n >= 2 ? lds8(s, at + 1) : 0u;
+__device__ __forceinline__ int ip_opt_len(uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
     switch (t) {
         case 0: kind = 0; return 1;
         case 1: kind = 1; return 1;
@@ -1531,12 +1546,15 @@ __device__ __forceinline__ int ip_opt_len(const uint8_t* s, uint32_t at, uint32_
         default: return -1;
     }
 }
-__device__ __forceinline__ uint32_t lds_be16(const uint8_t* s, uint32_t a) {
-    return (lds8(s, a) << 8) | lds8(s, a + 1);
-}
-__device__ __forceinline__ uint32_t lds_be32(const uint8_t* s, uint32_t a) {
-    return (lds8(s, a) << 24) | (lds8(s, a + 1) << 16) | (lds8(s, a + 2) << 8) | lds8(s, a + 3);
-}
+
+// One step of a TLV walk (state of Ipv4OptionsIter / TcpOptionsIter): the two walks of
+// a frame are independent, so the kernel steps both in one loop and their LDS round
+// trips overlap.
+struct OptWalk {
+    uint32_t lo, nb, pos, cnt, kinds, stop;
+    uint64_t trace;
+    bool on;
+};
 
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
@@ -1601,11 +1619,10 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         for (int k = 0; k < kOptChunks; ++k) {
             const int c = k * kWave + lane;
             const int q = c / kOptChunks, j = c % kOptChunks;
-            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
             const uint32_t lo = (uint32_t)__shfl((int)(need ? fr.off + need_lo : 0u), q, kWave);
             const uint32_t hi = (uint32_t)__shfl((int)(need ? fr.off + need_hi : 0u), q, kWave);
-            const uint32_t a = (qo & ~15u) + 16u * j;
-            addr[k] = (a < hi && a + 16u > lo) ? a : fb;
+            const uint32_t a = (lo & ~15u) + 16u * j;
+            addr[k] = a < hi ? a : fb;
             fix |= (uint32_t)straddles(addr[k], fb) << k;
         }
 #pragma unroll
@@ -1626,75 +1643,80 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     wave_sync();
 
     // the two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
-    // TcpOptionsIter::next, tcp/generated.rs:1400-1484)
-    const uint8_t* s = &W.win[lane * kOptSlot] + (fr.off & 15u);
+    // TcpOptionsIter::next, tcp/generated.rs:1400-1484), stepped together
+    const OptWin s{&W.win[lane * kOptSlot], ((fr.off + need_lo) & 15u) - need_lo};
     uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0;
-    uint64_t ip_trace = 0, tcp_trace = 0;
-    if (ip_parsed) {
-        uint32_t pos = 0, cnt = 0, kinds = 0, stop = RPKT_OPT_END;
-        const uint32_t nb = ip_hi - ip_lo;
-        while (pos < nb) {
+    OptWalk ip{ip_lo, ip_hi - ip_lo, 0, 0, 0, RPKT_OPT_END, 0, ip_parsed && ip_hi > ip_lo};
+    OptWalk tw{t_lo, t_hi - t_lo, 0, 0, 0, RPKT_OPT_END, 0, tcp && t_hi > t_lo};
+    while (ip.on || tw.on) {
+        if (ip.on) {
+            const uint32_t at = ip.lo + ip.pos;
+            const uint32_t d0 = s.dw(at);
             int kind = 0;
-            const int used = ip_opt_len(s, ip_lo + pos, nb - pos, kind);
+            const int used = ip_opt_len(d0, ip.nb - ip.pos, kind);
             if (used <= 0) {
-                stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
-                break;
+                ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                ip.on = false;
+            } else {
+                if (kind == 2) o[9] = (o[9] & 0xff000000u) | (d0 >> 8);
+                if (kind == 3) o[8] = (o[8] & 0xffffu) | ((d0 >> 8) << 16);
+                if (kind == 4) o[8] = (o[8] & 0xffff0000u) | be16_hi(d0);
+                if (kind == 5) o[11] = s.be32(at + 2);
+                if (kind == 6 || kind == 7) {
+                    o[9] = (o[9] & 0x00ffffffu) | ((d0 >> 16) << 24);
+                    o[10] = s.be32(at + 3);
+                }
+                ip.kinds |= 1u << kind;
+                if (ip.cnt < 16) ip.trace |= (uint64_t)(kind + 1) << (4 * ip.cnt);
+                ip.cnt += 1;
+                ip.pos += (uint32_t)used;
+                ip.on = ip.pos < ip.nb;
             }
-            const uint32_t at = ip_lo + pos;
-            if (kind == 2) o[9] = (o[9] & 0xff000000u) | lds8(s, at + 1) |
-                                  (lds8(s, at + 2) << 8) | (lds8(s, at + 3) << 16);
-            if (kind == 3) o[8] = (o[8] & 0xffffu) | (lds8(s, at + 1) << 16) | (lds8(s, at + 2) << 24);
-            if (kind == 4) o[8] = (o[8] & 0xffff0000u) | lds_be16(s, at + 2);
-            if (kind == 5) o[11] = lds_be32(s, at + 2);
-            if (kind == 6 || kind == 7) {
-                o[9] = (o[9] & 0x00ffffffu) | (lds8(s, at + 2) << 24);
-                o[10] = lds_be32(s, at + 3);
-            }
-            kinds |= 1u << kind;
-            if (cnt < 16) ip_trace |= (uint64_t)(kind + 1) << (4 * cnt);
-            cnt += 1;
-            pos += (uint32_t)used;
         }
+        if (tw.on) {
+            const uint32_t at = tw.lo + tw.pos;
+            const uint32_t d0 = s.dw(at);
+            int kind = 0;
+            const int used = tcp_opt_len(d0, tw.nb - tw.pos, kind);
+            if (used <= 0) {
+                tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                tw.on = false;
+            } else {
+                if (kind == 2) o[1] = (o[1] & 0xffffu) | (be16_hi(d0) << 16);
+                if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (((d0 >> 16) & 0xffu) << 16);
+                if (kind == 5) {
+                    const uint32_t hl = (d0 >> 8) & 0xffu;
+                    o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
+                    o[4] = hl >= 6u ? s.be32(at + 2) : 0u;
+                    o[5] = hl >= 10u ? s.be32(at + 6) : 0u;
+                }
+                if (kind == 6) {
+                    o[2] = s.be32(at + 2);
+                    o[3] = s.be32(at + 6);
+                }
+                if (kind == 7) o[6] = (o[6] & 0xffff0000u) | ((d0 >> 8) & 0xffu);
+                tw.kinds |= 1u << kind;
+                if (tw.cnt < 16) tw.trace |= (uint64_t)(kind + 1) << (4 * tw.cnt);
+                tw.cnt += 1;
+                tw.pos += (uint32_t)used;
+                tw.on = tw.pos < tw.nb;
+            }
+        }
+    }
+    if (ip_parsed) {
         // word 6: tcp_fo_len | tcp_end << 16 | ip_end << 24; word 7: ip_count | ip_stop << 8 | ip_kinds << 16
-        o[6] |= pos << 24;
-        o[7] = cnt | (stop << 8) | (kinds << 16);
+        o[6] |= ip.pos << 24;
+        o[7] = ip.cnt | (ip.stop << 8) | (ip.kinds << 16);
     }
     if (tcp) {
-        uint32_t pos = 0, cnt = 0, kinds = 0, stop = RPKT_OPT_END;
-        const uint32_t nb = t_hi - t_lo;
-        while (pos < nb) {
-            int kind = 0;
-            const int used = tcp_opt_len(s, t_lo + pos, nb - pos, kind);
-            if (used <= 0) {
-                stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
-                break;
-            }
-            const uint32_t at = t_lo + pos;
-            if (kind == 2) o[1] = (o[1] & 0xffffu) | (lds_be16(s, at + 2) << 16);
-            if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (lds8(s, at + 2) << 16);
-            if (kind == 5) {
-                const uint32_t hl = lds8(s, at + 1);
-                o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
-                o[4] = hl >= 6u ? lds_be32(s, at + 2) : 0u;
-                o[5] = hl >= 10u ? lds_be32(s, at + 6) : 0u;
-            }
-            if (kind == 6) {
-                o[2] = lds_be32(s, at + 2);
-                o[3] = lds_be32(s, at + 6);
-            }
-            if (kind == 7) o[6] = (o[6] & 0xffff0000u) | lds8(s, at + 1);
-            kinds |= 1u << kind;
-            if (cnt < 16) tcp_trace |= (uint64_t)(kind + 1) << (4 * cnt);
-            cnt += 1;
-            pos += (uint32_t)used;
-        }
         // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24; word 1: kinds | mss << 16
-        o[0] = (o[0] & 0xffff0000u) | cnt | (stop << 8);
-        o[1] = (o[1] & 0xffff0000u) | kinds;
-        o[6] = (o[6] & 0xff00ffffu) | (pos << 16);
+        o[0] = (o[0] & 0xffff0000u) | tw.cnt | (tw.stop << 8);
+        o[1] = (o[1] & 0xffff0000u) | tw.kinds;
+        o[6] = (o[6] & 0xff00ffffu) | (tw.pos << 16);
     }
+    const uint64_t tcp_trace = tw.trace, ip_trace = ip.trace;
     o[12] = (uint32_t)tcp_trace;
     o[13] = (uint32_t)(tcp_trace >> 32);
     o[14] = (uint32_t)ip_trace;
