@@ -1556,6 +1556,26 @@ struct OptWalk {
     bool on;
 };
 
+// A run of one-byte options of one type (EOL = kind 0, NOP = kind 1 in both iterators:
+// each is an option of length 1 and the walk goes on) is consumed up to four at a
+// time from the dword at the cursor: padding runs are most of a walk's steps.
+__device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
+    const uint32_t t0 = d0 & 0xffu;
+    if (t0 > 1u) return false;
+    const uint32_t x = d0 ^ (t0 * 0x01010101u);         // zero bytes: the same type
+    uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+    k = k < w.nb - w.pos ? k : w.nb - w.pos;            // >= 1: byte 0 matches
+    w.kinds |= 1u << t0;
+    if (w.cnt < 16) {
+        const uint64_t nib = (uint64_t)((t0 + 1u) * 0x1111u) & ((1ull << (4 * k)) - 1);
+        w.trace |= nib << (4 * w.cnt);
+    }
+    w.cnt += k;
+    w.pos += k;
+    w.on = w.pos < w.nb;
+    return true;
+}
+
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -1655,8 +1675,9 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             const uint32_t at = ip.lo + ip.pos;
             const uint32_t d0 = s.dw(at);
             int kind = 0;
-            const int used = ip_opt_len(d0, ip.nb - ip.pos, kind);
-            if (used <= 0) {
+            const int used = opt_run(ip, d0) ? -2 : ip_opt_len(d0, ip.nb - ip.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
                 ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
                 ip.on = false;
             } else {
@@ -1679,8 +1700,9 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             const uint32_t at = tw.lo + tw.pos;
             const uint32_t d0 = s.dw(at);
             int kind = 0;
-            const int used = tcp_opt_len(d0, tw.nb - tw.pos, kind);
-            if (used <= 0) {
+            const int used = opt_run(tw, d0) ? -2 : tcp_opt_len(d0, tw.nb - tw.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
                 tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
                 tw.on = false;
             } else {
