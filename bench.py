@@ -410,7 +410,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 7])
-    ap.add_argument("--also", default="3,4,7", help="extra configs reported under 'extra'")
+    ap.add_argument("--also", default="3,4,5,7", help="extra configs reported under 'extra'")
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
