@@ -45,6 +45,7 @@ constexpr int kSlot = kWin + 4;      // LDS slot stride: 33 dwords, so lane-stri
                                      // reads of the 64 slots hit 32 distinct banks
 constexpr int kStreamUnroll = 4;     // 16-B chunk loads in flight per lane per step
 constexpr uint64_t kMaxFrameBytes = 0xffffff00ull;  // voffset + 16 never wraps
+constexpr uint32_t kSplitStreamBytes = 65536;  // tile stream above which edge lines go first
 
 struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit a CU
     uint8_t  win[kWave * kSlot];     // header windows, slot stride 132 B
@@ -124,6 +125,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
     x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    return __builtin_amdgcn_readlane(wave_incl_scan(x), 63);
 }
 
 // propagate_carries (checksum.rs:115-118) for any u32 partial: 0 iff x == 0.
@@ -662,7 +667,7 @@ struct SpanSrc {
 // L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
 // tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
-// 22 = default-policy stream loads).
+// 22 = default-policy stream loads, 23 / 24 = edge lines first always / never).
 template <bool L4, int V>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
@@ -717,9 +722,25 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     // 3. L4 bytes beyond the window: flattened chunk stream over the tile
     if (L4 && V != 1) {
         // the L4 stream is read once: non-temporal loads (measured -13 % at 1500 B);
-        // the header windows keep the default policy (nt there measured slower)
-        const uint32_t sp = wave_stream_sum<(V == 22) ? 0 : 2>(
-            rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
+        // the header windows keep the default policy (nt there measured slower).
+        // A frame's stream shares a 128-B line with its own window (the line the window
+        // ends in) and, at its end, with the next frame's window.  On a long tile the
+        // stream reaches those lines tens of microseconds after the window loads, long
+        // after L2 dropped them, so they were fetched from HBM twice (+10-14 % traffic
+        // at 1500 B).  Long tiles therefore stream each range's partial head and tail
+        // lines first, while the window lines are hot, and the line-aligned middles last.
+        uint32_t sp;
+        const uint32_t ss = L.stream_s, se = L.stream_e;
+        const uint32_t tile_bytes = wave_sum(se - ss);
+        if ((V == 23 || tile_bytes > kSplitStreamBytes) && V != 24) {
+            const uint32_t h1 = min(se, (ss + 127u) & ~127u);
+            const uint32_t t0 = max(se & ~127u, h1);
+            sp = wave_stream_sum<0>(rs, frames_bytes, ss, h1, W, lane);
+            sp += wave_stream_sum<0>(rs, frames_bytes, t0, se, W, lane);
+            sp += wave_stream_sum<(V == 22) ? 0 : 2>(rs, frames_bytes, h1, t0, W, lane);
+        } else {
+            sp = wave_stream_sum<(V == 22) ? 0 : 2>(rs, frames_bytes, ss, se, W, lane);
+        }
         if (L.want_l4) {
             const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
             rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
@@ -2524,6 +2545,8 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 8: return RPKT_V(8);
         case 21: return RPKT_V(21);
         case 22: return RPKT_V(22);
+        case 23: return RPKT_V(23);
+        case 24: return RPKT_V(24);
         case 10:
             return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
