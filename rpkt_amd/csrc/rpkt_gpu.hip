@@ -434,19 +434,24 @@ __device__ __forceinline__ void read_hdr(const uint8_t* slot, uint32_t ldsx, Hdr
     for (int k = 0; k < 5; ++k) h.F[k] = align_bytes(h.R[k + 1], h.R[k], sh);
 }
 
-// Word sum of LDS bytes [s, e) using the already-read raw dwords R[0..N) at a0,
-// continuing with LDS reads past them (IPv4 options, long in-window L4 spans).
+// Word sum of LDS bytes [s, e) using the already-read raw dwords R[0..N) at
+// a0 = s & ~3, continuing with LDS reads past them (IPv4 options, long in-window L4
+// spans).  Whole dwords [a0, ceil4(e)) are summed unmasked, then the bytes of the
+// first dword below s and of the last dword from e on are subtracted (exact: they
+// were added): two masks per range instead of one per dword.
+__device__ __forceinline__ uint32_t low_bytes(uint32_t x, uint32_t n) {   // bytes [0, n), n <= 3
+    return x & ((1u << (8u * n)) - 1u);
+}
 template <int N>
 __device__ __forceinline__ uint32_t raw_range_sum(const uint8_t* slot, const uint32_t (&R)[N],
                                                   uint32_t a0, uint32_t s, uint32_t e) {
+    if (e <= s) return 0u;
     uint32_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int a = (int)(a0 + 4 * k);
-        acc += halves(R[k] & byte_mask((int)s - a, (int)e - a));
-    }
-    for (uint32_t a = a0 + 4 * N; a < e; a += 4)
-        acc += halves(lds32(slot, a) & byte_mask((int)s - (int)a, (int)e - (int)a));
+    for (int k = 0; k < N; ++k) acc = hsum(a0 + 4 * k < e ? R[k] : 0u, acc);
+    for (uint32_t a = a0 + 4 * N; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    acc -= halves(low_bytes(R[0], s & 3u));
+    if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
     return acc;
 }
 
@@ -1203,71 +1208,53 @@ __device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20]
     }
 }
 
-// Absolute-phase word sum of LDS slot bytes [s, e) (any alignment).
+// Absolute-phase word sum of LDS slot bytes [s, e) (any alignment): whole dwords,
+// minus the bytes of the first dword below s and of the last dword from e on.
 __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t s, uint32_t e) {
+    if (e <= s) return 0u;
     uint32_t acc = 0;
-    for (uint32_t a = s & ~3u; a < e; a += 4)
-        acc += halves(lds32(slot, a) & byte_mask((int)s - (int)a, (int)e - (int)a));
+    for (uint32_t a = s & ~3u; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    acc -= halves(low_bytes(lds32(slot, s & ~3u), s & 3u));
+    if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
     return acc;
 }
 
-// Store frame bytes [r0, r1) and [r2, r3) (frame-relative, per owning lane) from the
-// tile's LDS slots.  Ranges lie inside the LDS window (< kWin - phase).  Each owner
-// lane first publishes its frame offset and the 16-bit byte masks of its 8 window
-// chunks (W.pref / W.s, W.e, W.first, W.last: free once the stream is done); the
-// lane that stores chunk c = k*64 + lane then needs two LDS reads.  Stores: a full
-// chunk is one dwordx4, a full dword one dword, the rest byte by byte.
-__device__ __forceinline__ uint32_t range_mask16(int lo, int hi) {
-    const int l = lo < 0 ? 0 : lo, h = hi > 16 ? 16 : hi;
-    return h > l ? (((1u << h) - 1u) & ~((1u << l) - 1u)) : 0u;
-}
-
+// Store frame bytes [0, r1) (frame-relative, per owning lane) from the tile's LDS
+// slots.  The range lies inside the LDS window (r1 <= kWin - phase).  Each owner lane
+// publishes its frame offset and r1 (W.pref / W.s: free once the stream is done);
+// the lane that stores chunk c = k*64 + lane (piece j = lane & 7 of frame k*8 +
+// lane/8) reads those two words and clips the chunk against the range itself.  A
+// full chunk is one dwordx4, a full dword one dword, the rest byte by byte.
 __device__ __forceinline__ void write_back(uint8_t* frames, WaveScratch& W, int lane,
-                                           uint32_t off, uint32_t r0, uint32_t r1, uint32_t r2,
-                                           uint32_t r3) {
-    {
-        const int ph = (int)(off & 15u);
-        uint32_t M[4];
-#pragma unroll
-        for (int j = 0; j < kWinChunks; j += 2) {
-            const int b0 = 16 * j - ph, b1 = 16 * (j + 1) - ph;   // chunk starts, frame-relative
-            const uint32_t m0 = range_mask16((int)r0 - b0, (int)r1 - b0) |
-                                range_mask16((int)r2 - b0, (int)r3 - b0);
-            const uint32_t m1 = range_mask16((int)r0 - b1, (int)r1 - b1) |
-                                range_mask16((int)r2 - b1, (int)r3 - b1);
-            M[j / 2] = m0 | (m1 << 16);
-        }
-        W.s[lane] = M[0];
-        W.e[lane] = M[1];
-        W.first[lane] = M[2];
-        W.last[lane] = M[3];
-        W.pref[lane] = off;
-    }
+                                           uint32_t off, uint32_t r1) {
+    W.pref[lane] = off;
+    W.s[lane] = r1;
     wave_sync();
+    const int j = lane & (kWinChunks - 1);
 #pragma unroll
     for (int k = 0; k < kWinChunks; ++k) {
-        const int c = k * kWave + lane;
-        const int q = c / kWinChunks, j = c % kWinChunks;
-        const uint32_t mw = (j / 2 == 0) ? W.s[q] : (j / 2 == 1) ? W.e[q]
-                          : (j / 2 == 2) ? W.first[q] : W.last[q];
-        const uint32_t m = (mw >> (16 * (j & 1))) & 0xffffu;
-        if (!m) continue;
-        const uint32_t base = (W.pref[q] & ~15u) + 16u * j;        // chunk's absolute address
+        const int q = k * (kWave / kWinChunks) + lane / kWinChunks;
+        const uint32_t oq = W.pref[q], rq = W.s[q];
+        const int lo = (int)(oq & 15u) - 16 * j;          // chunk-relative frame start
+        const int hi = lo + (int)rq;                       // chunk-relative range end
+        if (rq == 0 || hi <= 0) continue;
+        const uint32_t base = (oq & ~15u) + 16u * j;       // chunk's absolute address
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&W.win[q * kSlot + 16 * j]);
-        if (m == 0xffffu) {
+        if (lo <= 0 && hi >= 16) {
             *reinterpret_cast<u32x4*>(frames + base) = u32x4{src[0], src[1], src[2], src[3]};
             continue;
         }
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-            const uint32_t dm = (m >> (4 * d)) & 15u;
-            if (dm == 15u) {
+            const int dl = lo - 4 * d, dh = hi - 4 * d;     // dword-relative range
+            if (dh <= 0 || dl >= 4) continue;
+            if (dl <= 0 && dh >= 4) {
                 *reinterpret_cast<uint32_t*>(frames + base + 4 * d) = src[d];
-            } else if (dm) {
+            } else {
                 const uint32_t v = src[d];
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    if (dm & (1u << b)) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
+                    if (b >= dl && b < dh) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
             }
         }
     }
@@ -1398,7 +1385,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     // the window holds the original bytes around the headers: round the written range
     // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
     const uint32_t r1 = ok ? line_end(fr, l4 + fixed4) : 0u;
-    write_back(frames, W, lane, fr.off, 0u, r1, 0u, 0u);
+    write_back(frames, W, lane, fr.off, r1);
     if (built && valid) built[i] = ok ? 1 : 0;
 }
 
@@ -1410,6 +1397,9 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
 // full recompute bit for bit (the oracle recomputes in full).  The written range is
 // rounded up to whole 16-B chunks inside the frame (the window holds the original
 // payload bytes), so a 64-B frame is rewritten with three dwordx4 stores.
+// V: ablation variant for tools/ablate.py (0 = the product kernel; 1 = no write-back,
+// 2 = parse without the L4 sum, 3 = window + write-back of the whole frame only).
+template <int V>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
 void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
                     uint32_t stride, uint32_t frame_len, uint32_t n, rpkt_fwd_t fwd,
@@ -1432,8 +1422,13 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         window_commit(W, rs, fb, d, addr, fix, lane);
     }
     wave_sync();
+    if constexpr (V == 3) {
+        write_back(frames, W, lane, fr.off, valid ? line_end(fr, 0u) : 0u);
+        if (valid) keep[i] = 1;
+        return;
+    }
     LaneRec L;
-    parse_lane(W, lane, fr, valid, RPKT_F_IP_SUM | RPKT_F_L4_SUM, L);
+    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L);
     uint8_t* slot = &W.win[lane * kSlot];
     uint8_t* s = slot + (fr.off & 15u);
     {
@@ -1504,7 +1499,7 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         r1 = line_end(fr, l4 + 8u);
     }
     wave_sync();
-    write_back(frames, W, lane, fr.off, 0u, r1, 0u, 0u);
+    if constexpr (V != 1) write_back(frames, W, lane, fr.off, r1);
     if (valid) keep[i] = fwd_ok ? 1 : 0;
 }
 
@@ -2489,9 +2484,30 @@ int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(forward_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    return launch(forward_kernel<0>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
                   b->stride, flen, b->n, *fwd, keep_dev);
+}
+
+// Development hook (not part of include/rpkt_gpu.h): forward_kernel ablation variants.
+int rpkt_gpu_debug_forward_variant(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
+                                   int variant, void* stream) {
+    if (!b || !fwd || !keep_dev || b->n == 0) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+#define RPKT_FV(v)                                                                          \
+    launch(forward_kernel<v>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,          \
+           const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,  \
+           b->stride, flen, b->n, *fwd, keep_dev)
+    switch (variant) {
+        case 0: return RPKT_FV(0);
+        case 1: return RPKT_FV(1);
+        case 2: return RPKT_FV(2);
+        case 3: return RPKT_FV(3);
+        default: return RPKT_E_INVAL;
+    }
+#undef RPKT_FV
 }
 
 int rpkt_gpu_options_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
