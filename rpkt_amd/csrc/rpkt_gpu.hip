@@ -2215,34 +2215,53 @@ void flow_hist_kernel(const uint64_t* __restrict__ ev, uint32_t n, uint32_t per_
     for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) out[r] = h[r];
 }
 
-// Slab reduce: block (x, y) sums slabs [y*kSlabGroup, (y+1)*kSlabGroup) for 256
-// buckets and adds the partial to the counters with u64 atomics (integer adds in any
-// order give the same bits, so the counters stay reproducible).
-constexpr uint32_t kSlabGroup = 16;
+// Slab reduce without atomics: block x owns buckets [64x, 64x + 64); its 16 waves
+// split the slabs (wave w sums slabs w, w + 16, ...; lane = bucket, so every load is
+// a coalesced 256-B row), the 16 partials meet in LDS, and wave 0 adds the totals to
+// the counters.  Each bucket has one writer, and integer sums in a fixed order give
+// the same bits every run.  (The earlier form, 16 slab groups per bucket joined by
+// u64 atomics, was atomic-bound: 18 us at 8M events; 4 groups 35 us, 64 groups 38 us.)
+constexpr uint32_t kReduceWaves = 16;
 
-__global__ void flow_reduce_kernel(const uint32_t* __restrict__ slab, uint32_t n_slabs,
-                                   uint32_t n_buckets, unsigned long long* __restrict__ counters) {
+__global__ __launch_bounds__(kWave * kReduceWaves)
+void flow_reduce_kernel(const uint32_t* __restrict__ slab, uint32_t n_slabs,
+                        uint32_t n_buckets, unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t part[kReduceWaves][5][kWave];     // pk, bytes lo, bytes hi, ipb, l4b
     const uint32_t rows = n_buckets + 1;
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= rows) return;
-    const uint32_t s0 = blockIdx.y * kSlabGroup;
-    const uint32_t s1 = min(n_slabs, s0 + kSlabGroup);
-    uint64_t pk = 0, by = 0, ipb = 0, l4b = 0;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint32_t b = blockIdx.x * kWave + lane;
+    uint32_t pk = 0, ipb = 0, l4b = 0;
+    uint64_t by = 0;
+    if (b < rows) {
 #pragma unroll 4
-    for (uint32_t s = s0; s < s1; ++s) {
-        const uint32_t* sl = slab + (size_t)s * 3 * rows;
-        pk += sl[b];
-        by += sl[rows + b];
-        const uint32_t bad = sl[2 * rows + b];
-        ipb += bad & 0xffffu;
-        l4b += bad >> 16;
+        for (uint32_t s = w; s < n_slabs; s += kReduceWaves) {
+            const uint32_t* sl = slab + (size_t)s * 3 * rows;
+            pk += sl[b];
+            by += sl[rows + b];
+            const uint32_t bad = sl[2 * rows + b];
+            ipb += bad & 0xffffu;
+            l4b += bad >> 16;
+        }
     }
-    if (pk) {
-        atomicAdd(&counters[4 * b + 0], (unsigned long long)pk);
-        atomicAdd(&counters[4 * b + 1], (unsigned long long)by);
+    part[w][0][lane] = pk;
+    part[w][1][lane] = (uint32_t)by;
+    part[w][2][lane] = (uint32_t)(by >> 32);
+    part[w][3][lane] = ipb;
+    part[w][4][lane] = l4b;
+    __syncthreads();
+    if (w != 0 || b >= rows) return;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kReduceWaves; ++k) {
+        t0 += part[k][0][lane];
+        t1 += part[k][1][lane] | ((uint64_t)part[k][2][lane] << 32);
+        t2 += part[k][3][lane];
+        t3 += part[k][4][lane];
     }
-    if (ipb) atomicAdd(&counters[4 * b + 2], (unsigned long long)ipb);
-    if (l4b) atomicAdd(&counters[4 * b + 3], (unsigned long long)l4b);
+    counters[4 * b + 0] += t0;
+    counters[4 * b + 1] += t1;
+    counters[4 * b + 2] += t2;
+    counters[4 * b + 3] += t3;
 }
 
 // n_buckets above the LDS limit: one global atomic set per event.
@@ -2623,8 +2642,8 @@ int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets
                     (const uint64_t*)ev, n, per, n_buckets, (uint32_t*)workspace);
     if (rc) return rc;
     const uint32_t rows = n_buckets + 1;
-    return launch(flow_reduce_kernel, dim3((rows + 255) / 256, (slabs + kSlabGroup - 1) / kSlabGroup),
-                  dim3(256), 0, st, (const uint32_t*)workspace, slabs, n_buckets,
+    return launch(flow_reduce_kernel, dim3((rows + kWave - 1) / kWave), dim3(kWave * kReduceWaves),
+                  0, st, (const uint32_t*)workspace, slabs, n_buckets,
                   (unsigned long long*)counters);
 }
 
