@@ -1818,68 +1818,124 @@ struct LayerWin {
     }
 };
 
-__device__ __forceinline__ uint32_t len_expr(const RpktLenExpr& e, uint32_t x) {
-    switch (e.form) {                           // pktfmt UsableAlgExpr (ast/length.rs:244-283)
+// The walk's LDS image of the table, repacked from kProtos / kGroups at kernel start
+// so that a protocol's scalars are two 16-B reads and a condition one: per protocol
+// 32 B, five 16-B condition slots, one dword per group.
+struct LayProto {
+    uint32_t a;               // hdr | hl_kind << 16 | pl_kind << 24
+    int32_t hl_fixed;
+    uint32_t hl0, hl1;        // expression: off | bits << 16 | form << 24 ; a | b << 16
+    uint32_t pl0, pl1;
+    uint32_t n_cond, pad;
+};
+struct LayCond {
+    uint32_t f;               // off | bits << 16 | n << 24
+    uint32_t lo01, hi01;      // lo[0] | lo[1] << 16 ; hi[0] | hi[1] << 16
+    uint32_t r2;              // lo[2] | hi[2] << 16
+};
+struct LayTable {
+    LayProto p[RPKT_N_PROTOS];
+    LayCond c[RPKT_N_PROTOS][5];
+    uint32_t g[RPKT_N_GROUPS];    // first | count << 8 | cond_bytes << 16
+};
+
+__device__ __forceinline__ void lay_table_fill(LayTable& T) {
+    for (uint32_t t = threadIdx.x; t < RPKT_N_PROTOS * 5; t += blockDim.x) {
+        const uint32_t id = t / 5, k = t % 5;
+        const RpktCond& C = kProtos[id].cond[k];
+        T.c[id][k] = LayCond{C.off | ((uint32_t)C.bits << 16) | ((uint32_t)C.n << 24),
+                             C.lo[0] | ((uint32_t)C.lo[1] << 16), C.hi[0] | ((uint32_t)C.hi[1] << 16),
+                             C.lo[2] | ((uint32_t)C.hi[2] << 16)};
+        if (k == 0) {
+            const RpktProto& P = kProtos[id];
+            T.p[id] = LayProto{P.hdr | ((uint32_t)P.hl_kind << 16) | ((uint32_t)P.pl_kind << 24),
+                               P.hl_fixed,
+                               P.hl.off | ((uint32_t)P.hl.bits << 16) | ((uint32_t)P.hl.form << 24),
+                               P.hl.a | ((uint32_t)P.hl.b << 16),
+                               P.pl.off | ((uint32_t)P.pl.bits << 16) | ((uint32_t)P.pl.form << 24),
+                               P.pl.a | ((uint32_t)P.pl.b << 16), P.n_cond, 0u};
+        }
+    }
+    if (threadIdx.x < RPKT_N_GROUPS) {
+        const RpktGroup G = kGroups[threadIdx.x];
+        T.g[threadIdx.x] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16);
+    }
+}
+
+// pktfmt UsableAlgExpr (ast/length.rs:244-283) of the field at expression e0/e1
+__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, uint32_t s, uint32_t e0,
+                                            uint32_t e1) {
+    const uint32_t x = Wn.field(s, e0 & 0xffffu, (e0 >> 16) & 0xffu);
+    const uint32_t a = e1 & 0xffffu, b = e1 >> 16;
+    switch (e0 >> 24) {
         case 0: return x;
-        case 1: return x + e.a;
-        case 2: return x * e.a;
-        case 3: return (x + e.a) * e.b;
-        default: return x * e.a + e.b;
+        case 1: return x + a;
+        case 2: return x * a;
+        case 3: return (x + a) * b;
+        default: return x * a + b;
     }
 }
 
 // group_parse + parse + payload() of group g at cursor [s, e): returns the member
-// protocol (< 0 on Err) with its header length and the trimmed packet end.
-__device__ __forceinline__ int walk_group(const LayerWin& Wn, const RpktProto* __restrict__ protos,
-                                          const RpktGroup* __restrict__ groups, uint32_t g,
+// protocol (< 0 on Err) with its header length and the trimmed packet end.  A group
+// whose members have no conditions (cond_bytes 0: every group but Ether, VLAN, ICMPv4,
+// GRE, PPPoE and STP) takes its first member without entering the member loop.
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayTable& T, uint32_t g,
                                           uint32_t s, uint32_t e, uint32_t& hl, uint32_t& end) {
     const uint32_t r = e - s;
-    const RpktGroup G = groups[g];
-    if (r < G.cond_bytes) return -1;
-    int m = -1;
-    for (uint32_t k = 0; k < G.count && m < 0; ++k) {
-        const RpktProto& P = protos[G.first + k];
-        bool ok = true;
-        for (uint32_t c = 0; c < P.n_cond && ok; ++c) {
-            const RpktCond& C = P.cond[c];
-            const uint32_t v = Wn.field(s, C.off, C.bits);
-            bool in = false;
-            for (uint32_t q = 0; q < C.n; ++q) in |= (v >= C.lo[q] && v <= C.hi[q]);
-            ok = in;
+    const uint32_t G = T.g[g];
+    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = G >> 16;
+    if (r < cond_bytes) return -1;
+    int m = (int)first;
+    if (cond_bytes) {
+        m = -1;
+        for (uint32_t k = 0; k < count && m < 0; ++k) {
+            const uint32_t id = first + k;
+            const uint32_t nc = T.p[id].n_cond;
+            bool ok = true;
+            for (uint32_t c = 0; c < nc && ok; ++c) {
+                const LayCond C = T.c[id][c];
+                const uint32_t v = Wn.field(s, C.f & 0xffffu, (C.f >> 16) & 0xffu);
+                const uint32_t n = C.f >> 24;
+                bool in = v >= (C.lo01 & 0xffffu) && v <= (C.hi01 & 0xffffu);
+                if (n > 1) in |= v >= (C.lo01 >> 16) && v <= (C.hi01 >> 16);
+                if (n > 2) in |= v >= (C.r2 & 0xffffu) && v <= (C.r2 >> 16);
+                ok = in;
+            }
+            if (ok) m = (int)id;
         }
-        if (ok) m = (int)(G.first + k);
+        if (m < 0) return -1;
     }
-    if (m < 0) return -1;
-    const RpktProto& P = protos[m];
-    if (r < P.hdr) return -1;
-    uint32_t h = P.hdr;
-    if (P.hl_kind == 1) {
-        h = len_expr(P.hl, Wn.field(s, P.hl.off, P.hl.bits));
-    } else if (P.hl_kind == 2 || P.hl_kind == 3) {         // gre/mod.rs:68-101
+    const LayProto P = T.p[m];
+    const uint32_t hdr = P.a & 0xffffu, hk = (P.a >> 16) & 0xffu, pk = P.a >> 24;
+    if (r < hdr) return -1;
+    uint32_t h = hdr;
+    if (hk == 1) {
+        h = lay_len(Wn, s, P.hl0, P.hl1);
+    } else if (hk == 2 || hk == 3) {                        // gre/mod.rs:68-101
         const uint32_t ind = Wn.be16(s);
-        h = P.hl_kind == 2
-                ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
-                      ((ind & 0x1000u) ? 4u : 0u)
-                : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
-    } else if (P.hl_kind == 4) {                            // gtpv1.pktfmt header_len
+        h = hk == 2 ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
+                          ((ind & 0x1000u) ? 4u : 0u)
+                    : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
+    } else if (hk == 4) {                                   // gtpv1.pktfmt header_len
         h = (Wn.at(s) & 7u) ? 12u : 8u;
-    } else if (P.hl_kind == 5) {                            // gtpv2.pktfmt header_len
+    } else if (hk == 5) {                                   // gtpv2.pktfmt header_len
         h = (Wn.at(s) & 8u) ? 12u : 8u;
     }
-    if (P.hl_kind) {
+    if (hk) {
         if (P.hl_fixed >= 0) {
             if (h != (uint32_t)P.hl_fixed) return -1;
-        } else if (h < P.hdr || h > r) {
+        } else if (h < hdr || h > r) {
             return -1;
         }
     }
     end = e;
-    if (P.pl_kind == 1) {                                   // payload_len
-        const uint32_t pay = len_expr(P.pl, Wn.field(s, P.pl.off, P.pl.bits));
+    if (pk == 1) {                                          // payload_len
+        const uint32_t pay = lay_len(Wn, s, P.pl0, P.pl1);
         if ((uint64_t)pay + h > r) return -1;
         end = s + h + pay;
-    } else if (P.pl_kind == 2) {                            // packet_len
-        const uint32_t pkt = len_expr(P.pl, Wn.field(s, P.pl.off, P.pl.bits));
+    } else if (pk == 2) {                                   // packet_len
+        const uint32_t pkt = lay_len(Wn, s, P.pl0, P.pl1);
         if (pkt < h || pkt > r) return -1;
         end = s + pkt;
     }
@@ -1981,15 +2037,9 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     // the protocol table in LDS: lanes walk different protocols, so table reads are
     // per-lane (divergent) loads; from LDS they cost tens of cycles instead of a
     // global-memory round trip per dependent lookup
-    __shared__ __attribute__((aligned(16))) RpktProto protos[RPKT_N_PROTOS];
-    __shared__ __attribute__((aligned(16))) RpktGroup groups[RPKT_N_GROUPS];
-    {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(kProtos);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(protos);
-        for (uint32_t k = threadIdx.x; k < sizeof(kProtos) / 4; k += blockDim.x) dst[k] = src[k];
-        if (threadIdx.x < RPKT_N_GROUPS) groups[threadIdx.x] = kGroups[threadIdx.x];
-        __syncthreads();
-    }
+    __shared__ __attribute__((aligned(16))) LayTable T;
+    lay_table_fill(T);
+    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     LayScratch& W = scratch[wid];
@@ -2044,7 +2094,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             break;
         }
         uint32_t hl = 0, end = 0;
-        const int p = walk_group(Wn, protos, groups, (uint32_t)g, s, e, hl, end);
+        const int p = walk_group(Wn, T, (uint32_t)g, s, e, hl, end);
         if (p < 0) {
             stop = RPKT_L_ERR;
             err_g = (uint32_t)g;
