@@ -2190,14 +2190,19 @@ void read_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, uint32_t* __re
 // tile's span (64 x stride); the last tile is clipped.
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
-                        uint32_t tile_bytes, uint32_t n, u32x4* __restrict__ out) {
+                        const uint32_t* __restrict__ offsets, uint32_t tile_bytes, uint32_t n,
+                        u32x4* __restrict__ out) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t t = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const uint32_t p0 = t * kWave;
     if (p0 >= n) return;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
-    const uint32_t s = t * tile_bytes;
-    const uint32_t e = s + tile_bytes < frames_bytes ? s + tile_bytes : frames_bytes;
+    uint32_t s = t * tile_bytes, e = s + tile_bytes;
+    if (offsets) {                                   // packed: the tile's frames' span
+        s = offsets[p0];
+        e = offsets[p0 + kWave < n ? p0 + kWave : n];
+    }
+    e = e < frames_bytes ? e : frames_bytes;
     u32x4 acc = {0u, 0u, 0u, 0u};
     for (uint32_t a = (s & ~15u) + 16u * lane; a < e; a += 16u * kWave * 8) {
         u32x4 x[8];
@@ -2649,9 +2654,9 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
                           (uint32_t*)recs);
         case 15:
-            if (b->offsets_dev || b->n == 0) return RPKT_E_INVAL;
             return launch(tile_rw_ref_kernel, dim3(grid), dim3(per_block), 0, st, b->frames_dev,
-                          (uint32_t)b->frames_bytes, b->stride * kWave, b->n, (u32x4*)recs);
+                          (uint32_t)b->frames_bytes, b->offsets_dev, b->stride * kWave, b->n,
+                          (u32x4*)recs);
         case 13:
             return launch(copy_ref_kernel<8, false>, dim3(8192), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),

@@ -3,8 +3,8 @@
 Times, interleaved in one process (cdna_hip_programming.md §5.4 rule 24):
   v0 product kernel, v1 window only (no parse), v2 no L4 stream, v3 no record
   stores, v10 streaming-copy reference (same read + write bytes, coalesced), v14 grid-stride
-  read-only reference, v15 same-traffic tile reference (strided configs: each wave streams
-  its tile's bytes with nt loads and writes 64 records, no parse).
+  read-only reference, v15 same-traffic tile reference (each wave streams its tile's
+  bytes with nt loads and writes 64 records, no parse).
 Usage: python tools/ablate.py [--configs 2,3] [--rounds 5] [--launches 20]
 """
 import argparse
@@ -43,7 +43,7 @@ for cfg in [int(c) for c in args.configs.split(",")]:
     sp = ctypes.c_void_p(st.cuda_stream)
     times = {v: [] for v in variants}
     flags = gen.FLAGS[cfg]
-    cfg_variants = [v for v in variants if not (v == 15 and hbs[0].offsets is not None)]
+    cfg_variants = variants
     for rnd in range(args.rounds + 1):
         for v in cfg_variants:
             e0 = torch.cuda.Event(enable_timing=True)
