@@ -672,7 +672,8 @@ struct SpanSrc {
 // L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
 // tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
-// 22 = default-policy stream loads, 23 / 24 = edge lines first always / never).
+// 22 = default-policy stream loads, 23 = edge lines streamed first after the parse,
+// 24 = never, 25 = after the parse on long tiles).
 template <bool L4, int V>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
@@ -690,13 +691,35 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
     const SpanSrc spans{offsets, stride, frame_len, frames_bytes, n};
 
-    // 1. header windows -> LDS
+    // 1. header windows -> LDS.  A frame's L4 stream shares a 128-B line with its own
+    // window (the line the window ends in) and, at its end, with the next frame's
+    // window; the memory side fetches whole lines.  On a long tile the stream reaches
+    // those lines tens of microseconds after the window loads, when L2 no longer holds
+    // them, so they came from HBM twice (+10-14 % traffic at 1500 B).  Long tiles
+    // therefore sum each frame's partial head line [wend, he) and partial tail line
+    // [tb, fend) right after the window loads land, while those lines are in L2; after the parse, a frame whose L4 range is [wend, fend) streams only the
+    // line-aligned middle [he, tb), any other frame its whole range.
     const Frame fr = spans.get(i);
+    const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
+    bool pro = false;
+    uint32_t pro_sum = 0, mid_s = 0, mid_e = 0;
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
         const uint32_t fix = window_issue<(V == 21) ? 2 : 0>(rs, frames_bytes, fr, lane, d, addr);
         window_commit(W, rs, frames_bytes, d, addr, fix, lane);
+    }
+    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25) {
+        const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
+        if (wave_sum(span) > kSplitStreamBytes) {               // wave-uniform
+            pro = true;
+            const uint32_t he = span ? min((wend + 127u) & ~127u, fend) : 0u;
+            const uint32_t tb = span ? max(fend & ~127u, he) : 0u;
+            pro_sum = wave_stream_sum<0>(rs, frames_bytes, span ? wend : 0u, he, W, lane);
+            pro_sum += wave_stream_sum<0>(rs, frames_bytes, tb, span ? fend : 0u, W, lane);
+            mid_s = he;
+            mid_e = tb;
+        }
     }
     wave_sync();
 
@@ -713,43 +736,48 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     } else {
         parse_lane(W, lane, fr, valid, flags, L);
     }
+    if constexpr (V != 3) stage_record(W, lane, L.w);
 
-    if constexpr (V == 3) {                                       // ablation: 4 B per frame
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < 20; ++k) x ^= L.w[k];
-        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
-        if (L4) wave_stream_sum<2>(rs, frames_bytes, L.stream_s, L.stream_e, W, lane);
-        return;
-    }
-    stage_record(W, lane, L.w);
-
-    // 3. L4 bytes beyond the window: flattened chunk stream over the tile
+    // 3. L4 bytes beyond the window: flattened chunk stream over the tile.  The stream
+    // is read once: non-temporal loads (measured -13 % at 1500 B); the header windows
+    // keep the default policy (nt there measured slower).
     if (L4 && V != 1) {
-        // the L4 stream is read once: non-temporal loads (measured -13 % at 1500 B);
-        // the header windows keep the default policy (nt there measured slower).
-        // A frame's stream shares a 128-B line with its own window (the line the window
-        // ends in) and, at its end, with the next frame's window.  On a long tile the
-        // stream reaches those lines tens of microseconds after the window loads, long
-        // after L2 dropped them, so they were fetched from HBM twice (+10-14 % traffic
-        // at 1500 B).  Long tiles therefore stream each range's partial head and tail
-        // lines first, while the window lines are hot, and the line-aligned middles last.
+        constexpr int kAux = (V == 22) ? 0 : 2;
         uint32_t sp;
         const uint32_t ss = L.stream_s, se = L.stream_e;
-        const uint32_t tile_bytes = wave_sum(se - ss);
-        if ((V == 23 || tile_bytes > kSplitStreamBytes) && V != 24) {
+        if (pro) {                                                // wave-uniform
+            const bool fast = se > ss && ss == wend && se == fend;
+            sp = wave_stream_sum<kAux>(rs, frames_bytes, fast ? mid_s : ss, fast ? mid_e : se,
+                                       W, lane);
+            if (fast) sp += pro_sum;
+        } else if ((V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes))) {
+            // ablation: the same split taken after the parse
             const uint32_t h1 = min(se, (ss + 127u) & ~127u);
             const uint32_t t0 = max(se & ~127u, h1);
             sp = wave_stream_sum<0>(rs, frames_bytes, ss, h1, W, lane);
             sp += wave_stream_sum<0>(rs, frames_bytes, t0, se, W, lane);
-            sp += wave_stream_sum<(V == 22) ? 0 : 2>(rs, frames_bytes, h1, t0, W, lane);
+            sp += wave_stream_sum<kAux>(rs, frames_bytes, h1, t0, W, lane);
         } else {
-            sp = wave_stream_sum<(V == 22) ? 0 : 2>(rs, frames_bytes, ss, se, W, lane);
+            sp = wave_stream_sum<kAux>(rs, frames_bytes, ss, se, W, lane);
+        }
+        if constexpr (V == 3) {                                   // ablation: 4 B per frame
+            uint32_t x = sp;
+#pragma unroll
+            for (int k = 0; k < 20; ++k) x ^= L.w[k];
+            if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+            return;
         }
         if (L.want_l4) {
             const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
             rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
         }
+    }
+    if constexpr (V == 3) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 20; ++k) x ^= L.w[k];
+        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+        return;
     }
 
     // 4. records (+ flow events)
@@ -2637,6 +2665,7 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 22: return RPKT_V(22);
         case 23: return RPKT_V(23);
         case 24: return RPKT_V(24);
+        case 25: return RPKT_V(25);
         case 10:
             return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
