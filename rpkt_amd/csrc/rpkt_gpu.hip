@@ -311,6 +311,48 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
     return (nch ? W.last[lane] - W.first[lane] : 0) + edge;
 }
 
+// Edge lines first (long tiles).  A frame's L4 stream shares a 128-B line with its own
+// window (the line the window ends in) and, at its end, with the next frame's window;
+// the memory side fetches whole lines.  On a long tile the stream reaches those lines
+// tens of microseconds after the window loads, when L2 no longer holds them, so they
+// came from HBM twice (+10-14 % traffic at 1500 B).  edge_lines_first sums each
+// frame's partial head line [wend, he) and partial tail line [tb, fend) right after
+// the window loads land, while those lines are in L2; stream_rest then streams only
+// the line-aligned middle [he, tb) of a frame whose stream range is exactly
+// [wend, fend), and the whole range of any other frame.
+struct EdgeLines {
+    bool on;                                 // wave-uniform
+    uint32_t sum, mid_s, mid_e;
+};
+
+__device__ __forceinline__ EdgeLines edge_lines_first(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                      WaveScratch& W, int lane, bool valid,
+                                                      uint32_t wend, uint32_t fend) {
+    EdgeLines X{false, 0u, 0u, 0u};
+    const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
+    if (wave_sum(span) <= kSplitStreamBytes) return X;            // wave-uniform
+    X.on = true;
+    const uint32_t he = span ? min((wend + 127u) & ~127u, fend) : 0u;
+    const uint32_t tb = span ? max(fend & ~127u, he) : 0u;
+    X.sum = wave_stream_sum<0>(rs, fb, span ? wend : 0u, he, W, lane);
+    X.sum += wave_stream_sum<0>(rs, fb, tb, span ? fend : 0u, W, lane);
+    X.mid_s = he;
+    X.mid_e = tb;
+    return X;
+}
+
+template <int AUX>
+__device__ __forceinline__ uint32_t stream_rest(const EdgeLines& X, __amdgpu_buffer_rsrc_t rs,
+                                                uint32_t fb, uint32_t ss, uint32_t se,
+                                                uint32_t wend, uint32_t fend, WaveScratch& W,
+                                                int lane) {
+    if (!X.on) return wave_stream_sum<AUX>(rs, fb, ss, se, W, lane);
+    const bool fast = se > ss && ss == wend && se == fend;
+    const uint32_t sp = wave_stream_sum<AUX>(rs, fb, fast ? X.mid_s : ss, fast ? X.mid_e : se,
+                                             W, lane);
+    return fast ? sp + X.sum : sp;
+}
+
 struct Frame { uint32_t off, len; };
 
 __device__ __forceinline__ Frame frame_span(const uint32_t* offsets, uint32_t stride,
@@ -691,36 +733,18 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
     const SpanSrc spans{offsets, stride, frame_len, frames_bytes, n};
 
-    // 1. header windows -> LDS.  A frame's L4 stream shares a 128-B line with its own
-    // window (the line the window ends in) and, at its end, with the next frame's
-    // window; the memory side fetches whole lines.  On a long tile the stream reaches
-    // those lines tens of microseconds after the window loads, when L2 no longer holds
-    // them, so they came from HBM twice (+10-14 % traffic at 1500 B).  Long tiles
-    // therefore sum each frame's partial head line [wend, he) and partial tail line
-    // [tb, fend) right after the window loads land, while those lines are in L2; after the parse, a frame whose L4 range is [wend, fend) streams only the
-    // line-aligned middle [he, tb), any other frame its whole range.
+    // 1. header windows -> LDS (then, on long tiles, the edge lines: edge_lines_first)
     const Frame fr = spans.get(i);
     const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
-    bool pro = false;
-    uint32_t pro_sum = 0, mid_s = 0, mid_e = 0;
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
         const uint32_t fix = window_issue<(V == 21) ? 2 : 0>(rs, frames_bytes, fr, lane, d, addr);
         window_commit(W, rs, frames_bytes, d, addr, fix, lane);
     }
-    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25) {
-        const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
-        if (wave_sum(span) > kSplitStreamBytes) {               // wave-uniform
-            pro = true;
-            const uint32_t he = span ? min((wend + 127u) & ~127u, fend) : 0u;
-            const uint32_t tb = span ? max(fend & ~127u, he) : 0u;
-            pro_sum = wave_stream_sum<0>(rs, frames_bytes, span ? wend : 0u, he, W, lane);
-            pro_sum += wave_stream_sum<0>(rs, frames_bytes, tb, span ? fend : 0u, W, lane);
-            mid_s = he;
-            mid_e = tb;
-        }
-    }
+    EdgeLines X{false, 0u, 0u, 0u};
+    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25)
+        X = edge_lines_first(rs, frames_bytes, W, lane, valid, wend, fend);
     wave_sync();
 
     // 2. lane-per-frame parse
@@ -745,12 +769,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         constexpr int kAux = (V == 22) ? 0 : 2;
         uint32_t sp;
         const uint32_t ss = L.stream_s, se = L.stream_e;
-        if (pro) {                                                // wave-uniform
-            const bool fast = se > ss && ss == wend && se == fend;
-            sp = wave_stream_sum<kAux>(rs, frames_bytes, fast ? mid_s : ss, fast ? mid_e : se,
-                                       W, lane);
-            if (fast) sp += pro_sum;
-        } else if ((V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes))) {
+        if (V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes)) {
             // ablation: the same split taken after the parse
             const uint32_t h1 = min(se, (ss + 127u) & ~127u);
             const uint32_t t0 = max(se & ~127u, h1);
@@ -758,7 +777,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
             sp += wave_stream_sum<0>(rs, frames_bytes, t0, se, W, lane);
             sp += wave_stream_sum<kAux>(rs, frames_bytes, h1, t0, W, lane);
         } else {
-            sp = wave_stream_sum<kAux>(rs, frames_bytes, ss, se, W, lane);
+            sp = stream_rest<kAux>(X, rs, frames_bytes, ss, se, wend, fend, W, lane);
         }
         if constexpr (V == 3) {                                   // ablation: 4 B per frame
             uint32_t x = sp;
@@ -1354,6 +1373,9 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         load_records_tile(recs, p0, n, W, lane, w);             // window loads in flight
         window_commit(W, rs, fb, d, addr, fix, lane);
     }
+    const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
+    EdgeLines X{false, 0u, 0u, 0u};
+    if constexpr (L4FILL) X = edge_lines_first(rs, fb, W, lane, valid, wend, fend);
     wave_sync();
 
     const uint32_t ph = fr.off & 15u, len = fr.len;
@@ -1398,7 +1420,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         }
         *reinterpret_cast<uint32_t*>(slot + kWin) =
             (uint32_t)fill_l4 | ((uint32_t)(proto == 17u) << 1) | ((ph + l4) << 8);
-        const uint32_t sp = wave_stream_sum<2>(rs, fb, ss, se, W, lane);
+        const uint32_t sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
         const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
         if (info & 1u) {
             const uint32_t at = info >> 8;                      // slot offset of the L4 header
