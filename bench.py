@@ -168,6 +168,18 @@ def head_sample(hb, max_bytes=256 << 20):
                          hb.frame_len)
 
 
+def cpu_model():
+    """The host CPU's model name (SURVEY.md §8d asks for it beside the core count)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_chains(hc, gpu_recs, flags, seconds, max_bytes=256 << 20):
     """Chain oracle (oracle/rpkt_oracle_chain.c, 1 thread) over the first chains of
     the batch (~max_bytes of frame data); checks the GPU records of the sample."""
@@ -187,6 +199,7 @@ def cpu_baseline_chains(hc, gpu_recs, flags, seconds, max_bytes=256 << 20):
     nbytes = int(hc.lens()[:m].sum())
     return {
         "value": round(m * reps / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+        "cpu_model": cpu_model(),
         "gb_per_s": round(nbytes * reps / dt / 1e9, 3),
         "sample": "%d reps x first %d chains (%.0f MB, %d segments) of the batch, 1 thread, "
                   "%.1f s" % (reps, m, nbytes / 1e6, segs.shape[0], dt),
@@ -221,6 +234,7 @@ def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     parity = gpu_recs.tobytes() == o.tobytes()
     return {
         "value": round(frames_total / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+        "cpu_model": cpu_model(),
         "gb_per_s": round(bytes_total / dt / 1e9, 3),
         "sample": "%d reps x first %d frames (%.0f MB) of the batch, 1 thread, %.1f s" % (
             reps, n, int(hb.lens().sum()) / 1e6, dt),
