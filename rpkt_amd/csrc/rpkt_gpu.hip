@@ -1868,6 +1868,54 @@ struct LayerWin {
     }
 };
 
+// The first 20 bytes of the current header as frame-relative little-endian dwords,
+// read once per layer step: every condition, header_len and payload_len field of the
+// table but one (MSTP's, at byte 36) and every dispatch key of lay_next lies in them,
+// so a step costs one round of LDS reads instead of a dependent read per field.
+struct LayHdr {
+    uint32_t F[5];
+};
+
+__device__ __forceinline__ LayHdr lay_hdr(const LayerWin& Wn, uint32_t s) {
+    LayHdr H;
+    if (s + 20u <= Wn.avail) {
+        const uint32_t y = Wn.ph + s, a = y & ~3u;
+        uint32_t R[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) R[k] = lds32(Wn.base, a + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) H.F[k] = align_bytes(R[k + 1], R[k], y & 3u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) H.F[k] = Wn.dw(s + 4 * k);
+    }
+    return H;
+}
+// header bytes [x, x + 4), x <= 15
+__device__ __forceinline__ uint32_t hdr_dw(const LayHdr& H, uint32_t x) {
+    const uint32_t k = x >> 2;
+    uint32_t lo = H.F[0], hi = H.F[1];
+    lo = k == 1 ? H.F[1] : lo;
+    hi = k == 1 ? H.F[2] : hi;
+    lo = k == 2 ? H.F[2] : lo;
+    hi = k == 2 ? H.F[3] : hi;
+    lo = k == 3 ? H.F[3] : lo;
+    hi = k == 3 ? H.F[4] : hi;
+    return align_bytes(hi, lo, x & 3u);
+}
+__device__ __forceinline__ uint32_t hdr_be16(const LayHdr& H, uint32_t x) {
+    return be16_lo(hdr_dw(H, x));
+}
+__device__ __forceinline__ uint32_t hdr_at(const LayHdr& H, uint32_t x) {
+    return hdr_dw(H, x) & 0xffu;
+}
+// the big-endian bit field of the table at bit offset ob of header s (Wn.field's rule)
+__device__ __forceinline__ uint32_t hdr_field(const LayerWin& Wn, const LayHdr& H, uint32_t s,
+                                              uint32_t ob, uint32_t bits) {
+    if (__builtin_expect((ob >> 3) > 15u, 0)) return Wn.field(s, ob, bits);
+    return (bswap32(hdr_dw(H, ob >> 3)) << (ob & 7u)) >> (32u - bits);
+}
+
 // The walk's LDS image of the table, repacked from kProtos / kGroups at kernel start
 // so that a protocol's scalars are two 16-B reads and a condition one: per protocol
 // 32 B, five 16-B condition slots, one dword per group.
@@ -1913,9 +1961,9 @@ __device__ __forceinline__ void lay_table_fill(LayTable& T) {
 }
 
 // pktfmt UsableAlgExpr (ast/length.rs:244-283) of the field at expression e0/e1
-__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, uint32_t s, uint32_t e0,
-                                            uint32_t e1) {
-    const uint32_t x = Wn.field(s, e0 & 0xffffu, (e0 >> 16) & 0xffu);
+__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H, uint32_t s,
+                                            uint32_t e0, uint32_t e1) {
+    const uint32_t x = hdr_field(Wn, H, s, e0 & 0xffffu, (e0 >> 16) & 0xffu);
     const uint32_t a = e1 & 0xffffu, b = e1 >> 16;
     switch (e0 >> 24) {
         case 0: return x;
@@ -1930,8 +1978,9 @@ __device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, uint32_t s, uint
 // protocol (< 0 on Err) with its header length and the trimmed packet end.  A group
 // whose members have no conditions (cond_bytes 0: every group but Ether, VLAN, ICMPv4,
 // GRE, PPPoE and STP) takes its first member without entering the member loop.
-__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayTable& T, uint32_t g,
-                                          uint32_t s, uint32_t e, uint32_t& hl, uint32_t& end) {
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
+                                          uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
+                                          uint32_t& end) {
     const uint32_t r = e - s;
     const uint32_t G = T.g[g];
     const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = G >> 16;
@@ -1945,7 +1994,7 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayTable& T,
             bool ok = true;
             for (uint32_t c = 0; c < nc && ok; ++c) {
                 const LayCond C = T.c[id][c];
-                const uint32_t v = Wn.field(s, C.f & 0xffffu, (C.f >> 16) & 0xffu);
+                const uint32_t v = hdr_field(Wn, H, s, C.f & 0xffffu, (C.f >> 16) & 0xffu);
                 const uint32_t n = C.f >> 24;
                 bool in = v >= (C.lo01 & 0xffffu) && v <= (C.hi01 & 0xffffu);
                 if (n > 1) in |= v >= (C.lo01 >> 16) && v <= (C.hi01 >> 16);
@@ -1961,16 +2010,16 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayTable& T,
     if (r < hdr) return -1;
     uint32_t h = hdr;
     if (hk == 1) {
-        h = lay_len(Wn, s, P.hl0, P.hl1);
+        h = lay_len(Wn, H, s, P.hl0, P.hl1);
     } else if (hk == 2 || hk == 3) {                        // gre/mod.rs:68-101
-        const uint32_t ind = Wn.be16(s);
+        const uint32_t ind = hdr_be16(H, 0);
         h = hk == 2 ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
                           ((ind & 0x1000u) ? 4u : 0u)
                     : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
     } else if (hk == 4) {                                   // gtpv1.pktfmt header_len
-        h = (Wn.at(s) & 7u) ? 12u : 8u;
+        h = (hdr_at(H, 0) & 7u) ? 12u : 8u;
     } else if (hk == 5) {                                   // gtpv2.pktfmt header_len
-        h = (Wn.at(s) & 8u) ? 12u : 8u;
+        h = (hdr_at(H, 0) & 8u) ? 12u : 8u;
     }
     if (hk) {
         if (P.hl_fixed >= 0) {
@@ -1981,11 +2030,11 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayTable& T,
     }
     end = e;
     if (pk == 1) {                                          // payload_len
-        const uint32_t pay = lay_len(Wn, s, P.pl0, P.pl1);
+        const uint32_t pay = lay_len(Wn, H, s, P.pl0, P.pl1);
         if ((uint64_t)pay + h > r) return -1;
         end = s + h + pay;
     } else if (pk == 2) {                                   // packet_len
-        const uint32_t pkt = lay_len(Wn, s, P.pl0, P.pl1);
+        const uint32_t pkt = lay_len(Wn, H, s, P.pl0, P.pl1);
         if (pkt < h || pkt > r) return -1;
         end = s + pkt;
     }
@@ -2026,27 +2075,27 @@ __device__ __forceinline__ int lay_ipproto(uint32_t p) {
 
 // The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
 // starts at h; the cursor is now [s, e).
-__device__ __forceinline__ int lay_next(const LayerWin& Wn, int p, uint32_t h, uint32_t s,
+__device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, int p, uint32_t s,
                                         uint32_t e, uint32_t& key) {
     switch (p) {
-        case RPKT_P_ETHER_ETHERFRAME: key = Wn.be16(h + 12); return lay_ethertype(key);
-        case RPKT_P_VLAN_VLANFRAME: key = Wn.be16(h + 2); return lay_ethertype(key);
+        case RPKT_P_ETHER_ETHERFRAME: key = hdr_be16(H, 12); return lay_ethertype(key);
+        case RPKT_P_VLAN_VLANFRAME: key = hdr_be16(H, 2); return lay_ethertype(key);
         case RPKT_P_ETHER_ETHERDOT3FRAME: case RPKT_P_VLAN_VLANDOT3FRAME: return RPKT_G_LLC;
         case RPKT_P_IPV4_IPV4:
-            if (Wn.be16(h + 6) & 0x1fffu) return kNextEnd;          // non-first fragment
-            key = Wn.at(h + 9);
+            if (hdr_be16(H, 6) & 0x1fffu) return kNextEnd;          // non-first fragment
+            key = hdr_at(H, 9);
             return lay_ipproto(key);
-        case RPKT_P_IPV6_IPV6: key = Wn.at(h + 6); return lay_ipproto(key);
+        case RPKT_P_IPV6_IPV6: key = hdr_at(H, 6); return lay_ipproto(key);
         case RPKT_P_IPV6_FRAGMENTHEADER:
-            if (Wn.be16(h + 2) >> 3) return kNextEnd;
-            key = Wn.at(h);
+            if (hdr_be16(H, 2) >> 3) return kNextEnd;
+            key = hdr_at(H, 0);
             return lay_ipproto(key);
         case RPKT_P_IPV6_HOPBYHOPOPTION: case RPKT_P_IPV6_DESTOPTIONS:
         case RPKT_P_IPV6_ROUTINGHEADER: case RPKT_P_IPV6_AUTHENTICATIONHEADER:
-            key = Wn.at(h);
+            key = hdr_at(H, 0);
             return lay_ipproto(key);
         case RPKT_P_UDP_UDP: {
-            const uint32_t dp = Wn.be16(h + 2), sp = Wn.be16(h);
+            const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0);
             const uint32_t port = (dp == 4789u || dp == 2152u || dp == 2123u) ? dp
                                 : ((sp == 4789u || sp == 2152u || sp == 2123u) ? sp : 0u);
             if (!port) return kNextEnd;
@@ -2057,24 +2106,24 @@ __device__ __forceinline__ int lay_next(const LayerWin& Wn, int p, uint32_t h, u
             return key == 1u ? RPKT_G_GTPV1 : (key == 2u ? RPKT_G_GTPV2 : kNextUnknown);
         }
         case RPKT_P_GRE_GRE:
-            key = Wn.be16(h + 2);
+            key = hdr_be16(H, 2);
             return key == 0x6558u ? RPKT_G_ETHER : lay_ethertype(key);
         case RPKT_P_VXLAN_VXLAN: return RPKT_G_ETHER;
         case RPKT_P_GTPV1_GTPV1:
-            if ((Wn.at(h) & 4u) || Wn.at(h + 1) != 255u) return kNextEnd;
+            if ((hdr_at(H, 0) & 4u) || hdr_at(H, 1) != 255u) return kNextEnd;
             if (e <= s) return kNextEnd;
             key = Wn.at(s) >> 4;
             return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
         case RPKT_P_MPLS_MPLS:
-            if (!(Wn.at(h + 2) & 1u)) return RPKT_G_MPLS;
+            if (!(hdr_at(H, 2) & 1u)) return RPKT_G_MPLS;
             if (e <= s) return kNextEnd;
             key = Wn.at(s) >> 4;
             return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
         case RPKT_P_PPPOE_PPPOESESSION:
-            key = Wn.be16(h + 6);
+            key = hdr_be16(H, 6);
             return key == 0x0021u ? RPKT_G_IPV4 : (key == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
         case RPKT_P_LLC_LLC:
-            return (Wn.at(h) == 0x42u && Wn.at(h + 1) == 0x42u) ? RPKT_G_STP : kNextEnd;
+            return (hdr_at(H, 0) == 0x42u && hdr_at(H, 1) == 0x42u) ? RPKT_G_STP : kNextEnd;
         default: return kNextEnd;
     }
 }
@@ -2144,7 +2193,8 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             break;
         }
         uint32_t hl = 0, end = 0;
-        const int p = walk_group(Wn, T, (uint32_t)g, s, e, hl, end);
+        const LayHdr H = lay_hdr(Wn, s);
+        const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end);
         if (p < 0) {
             stop = RPKT_L_ERR;
             err_g = (uint32_t)g;
@@ -2153,12 +2203,11 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl
         o[4 + nl / 4] |= (uint32_t)p << (8 * (nl & 3));
         o[8 + nl / 2] |= s << (16 * (nl & 1));
-        const uint32_t h = s;
         nl += 1;
         e = end;
         s += hl;
         uint32_t k2 = 0;
-        const int nx = lay_next(Wn, p, h, s, e, k2);
+        const int nx = lay_next(Wn, H, p, s, e, k2);
         if (nx == kNextEnd) {
             stop = RPKT_L_END;
             break;
