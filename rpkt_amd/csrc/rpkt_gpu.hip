@@ -1934,7 +1934,9 @@ struct LayCond {
 struct LayTable {
     LayProto p[RPKT_N_PROTOS];
     LayCond c[RPKT_N_PROTOS][5];
-    uint32_t g[RPKT_N_GROUPS];    // first | count << 8 | cond_bytes << 16
+    uint32_t g[RPKT_N_GROUPS];    // first | count << 8 | cond_bytes << 16 | lut << 24
+    uint32_t lutf[RPKT_N_LUT];    // lookup groups: the keyed field, off | bits << 16
+    uint8_t lut[RPKT_N_LUT][256]; // field value -> member (0xff: none)
 };
 
 __device__ __forceinline__ void lay_table_fill(LayTable& T) {
@@ -1956,8 +1958,12 @@ __device__ __forceinline__ void lay_table_fill(LayTable& T) {
     }
     if (threadIdx.x < RPKT_N_GROUPS) {
         const RpktGroup G = kGroups[threadIdx.x];
-        T.g[threadIdx.x] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16);
+        T.g[threadIdx.x] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
+                           ((uint32_t)G.lut << 24);
     }
+    if (threadIdx.x < RPKT_N_LUT) T.lutf[threadIdx.x] = kGroupLutField[threadIdx.x];
+    for (uint32_t t = threadIdx.x; t < RPKT_N_LUT * 64; t += blockDim.x)
+        reinterpret_cast<uint32_t*>(T.lut)[t] = reinterpret_cast<const uint32_t*>(kGroupLut)[t];
 }
 
 // pktfmt UsableAlgExpr (ast/length.rs:244-283) of the field at expression e0/e1
@@ -1977,16 +1983,23 @@ __device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H,
 // group_parse + parse + payload() of group g at cursor [s, e): returns the member
 // protocol (< 0 on Err) with its header length and the trimmed packet end.  A group
 // whose members have no conditions (cond_bytes 0: every group but Ether, VLAN, ICMPv4,
-// GRE, PPPoE and STP) takes its first member without entering the member loop.
+// GRE, PPPoE and STP) takes its first member without entering the member loop; a
+// group keyed on one byte (ICMPv4 types, PPPoE codes) looks its member up.
 __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
                                           uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
                                           uint32_t& end) {
     const uint32_t r = e - s;
     const uint32_t G = T.g[g];
-    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = G >> 16;
+    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
+    const uint32_t lut = G >> 24;
     if (r < cond_bytes) return -1;
     int m = (int)first;
-    if (cond_bytes) {
+    if (lut != 0xffu) {                                      // one keyed field: table lookup
+        const uint32_t f = T.lutf[lut];
+        const uint32_t mm = T.lut[lut][hdr_field(Wn, H, s, f & 0xffffu, f >> 16)];
+        if (mm == 0xffu) return -1;
+        m = (int)mm;
+    } else if (cond_bytes) {
         m = -1;
         for (uint32_t k = 0; k < count && m < 0; ++k) {
             const uint32_t id = first + k;

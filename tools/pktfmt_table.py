@@ -230,7 +230,7 @@ def c_header(t):
          "    uint8_t n_cond;",
          "    RpktCond cond[5];",
          "};",
-         "struct RpktGroup { uint8_t first, count, cond_bytes; };", ""]
+         "struct RpktGroup { uint8_t first, count, cond_bytes, lut; };   // lut 0xff: none", ""]
     for g in t["groups"]:
         L.append("#define RPKT_G_%s %d" % (g["name"], t["groups"].index(g)))
     L.append("#define RPKT_N_GROUPS %d" % len(t["groups"]))
@@ -257,10 +257,36 @@ def c_header(t):
             -1 if p["hl_fixed"] is None else p["hl_fixed"], ex(p["hl"]), ex(p["pl"]),
             len(p["cond"]), ", ".join(conds), p["id"], p["spec"], p["name"]))
     L.append("};")
+    # Groups whose members each test one condition on the same field of <= 8 bits
+    # (ICMPv4 types, PPPoE codes) also get a 256-entry lookup: field value -> the
+    # first member whose ranges hold it (0xff: none), so a walk resolves them with one
+    # table read instead of a loop over the members.
+    luts = []
+    for g in t["groups"]:
+        ms = [t["packets"][i] for i in g["members"]]
+        f0 = ms[0]["cond"][0] if ms[0]["cond"] else None
+        if (len(ms) > 1 and f0 and f0["bits"] <= 8 and
+                all(len(m["cond"]) == 1 and m["cond"][0]["off"] == f0["off"] and
+                    m["cond"][0]["bits"] == f0["bits"] for m in ms)):
+            row = []
+            for v in range(256):
+                hit = [m["id"] for m in ms if any(lo <= v <= hi for lo, hi in m["cond"][0]["ranges"])]
+                row.append(hit[0] if hit else 0xFF)
+            g["lut"] = len(luts)
+            luts.append((f0["off"], f0["bits"], row))
+        else:
+            g["lut"] = 0xFF
+    L.append("#define RPKT_N_LUT %d" % len(luts))
+    L.append("__device__ __constant__ const uint32_t kGroupLutField[RPKT_N_LUT] = {%s};  // off | bits << 16" %
+             ", ".join("%d" % (o | (b << 16)) for o, b, _ in luts))
+    L.append("__device__ __constant__ const uint8_t kGroupLut[RPKT_N_LUT][256] = {")
+    for _, _, row in luts:
+        L.append("    {%s}," % ", ".join(str(x) for x in row))
+    L.append("};")
     L.append("__device__ __constant__ const RpktGroup kGroups[RPKT_N_GROUPS] = {")
     for g in t["groups"]:
-        L.append("    {%d, %d, %d},  // %s" % (g["members"][0], len(g["members"]),
-                                              g["cond_bytes"], g["name"]))
+        L.append("    {%d, %d, %d, %d},  // %s" % (g["members"][0], len(g["members"]),
+                                                  g["cond_bytes"], g["lut"], g["name"]))
     L.append("};")
     return "\n".join(L) + "\n"
 
@@ -294,6 +320,8 @@ def main(ref="/root/reference"):
         fh.write(c_header(t))
     with open(os.path.join(ROOT, "include", "rpkt_protocols.h"), "w") as fh:
         fh.write(host_header(t))
+    for g in t["groups"]:
+        g.pop("lut", None)
     with open(os.path.join(ROOT, "tests", "golden", "proto_table.json"), "w") as fh:
         json.dump(t, fh, indent=1)
     print("%d packets in %d groups" % (len(t["packets"]), len(t["groups"])))
