@@ -187,7 +187,10 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* batch, uint32_t flags,
 
 /* Accumulate flow events into counters_dev (u64[(n_buckets+1)*4], caller
  * zeroes it once; calls add).  workspace_dev must hold
- * rpkt_gpu_flow_workspace_bytes(n, n_buckets) bytes. */
+ * rpkt_gpu_flow_workspace_bytes(n, n_buckets) bytes.  Calls that add into the
+ * same counters (or share a workspace) must be ordered, e.g. on one stream: up
+ * to 8192 buckets each bucket is added by one thread without atomics, so the
+ * counters are bitwise reproducible. */
 size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets);
 int rpkt_gpu_flow_count(const rpkt_flow_ev_t* flow_ev_dev, uint32_t n,
                         uint32_t n_buckets, uint64_t* counters_dev,
