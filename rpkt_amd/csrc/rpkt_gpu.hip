@@ -1628,13 +1628,13 @@ struct OptWalk {
 __device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
     const uint32_t t0 = d0 & 0xffu;
     if (t0 > 1u) return false;
-    const uint32_t x = d0 ^ (t0 * 0x01010101u);         // zero bytes: the same type
+    const uint32_t x = d0 ^ (t0 ? 0x01010101u : 0u);   // zero bytes: the same type
     uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
     k = k < w.nb - w.pos ? k : w.nb - w.pos;            // >= 1: byte 0 matches
     w.kinds |= 1u << t0;
     if (w.cnt < 16) {
-        const uint64_t nib = (uint64_t)((t0 + 1u) * 0x1111u) & ((1ull << (4 * k)) - 1);
-        w.trace |= nib << (4 * w.cnt);
+        const uint32_t nib = (t0 ? 0x2222u : 0x1111u) & ((1u << (4 * k)) - 1u);   // k <= 4
+        w.trace |= (uint64_t)nib << (4 * w.cnt);
     }
     w.cnt += k;
     w.pos += k;
