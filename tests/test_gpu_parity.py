@@ -209,6 +209,23 @@ def test_checksum_ranges_match_from_slice(torch):
     assert got[:3000].tolist() == want
 
 
+def test_checksum_ranges_at_buffer_end(torch):
+    """Every (start, len) range inside the last 48 bytes of buffers whose size is not
+    a multiple of 16: the edge chunks of the stream straddle the descriptor's end
+    (the hardware drops such a dwordx4 whole; the kernel re-reads it), at every phase."""
+    rng = np.random.default_rng(21)
+    for size in (1001, 1024 + 7, 4093, 33, 7):
+        buf = rng.integers(0, 256, size, dtype=np.uint8)
+        lo = max(0, size - 48)
+        ranges = np.array([(s, l) for s in range(lo, size + 1) for l in range(0, size - s + 1)],
+                          dtype=np.uint32)
+        out = engine.checksum_ranges(torch.from_numpy(buf).cuda(),
+                                     torch.from_numpy(ranges.view(np.int32)).cuda())
+        got = out.cpu().numpy().view(np.uint16).tolist()
+        want = [oracle.from_slice(buf[s:s + l]) for s, l in ranges]
+        assert got == want, size
+
+
 def test_cpp_host_example_through_c_abi(torch):
     """examples/parse_batch: a non-Python host (plain hipMalloc) drives the C ABI."""
     import subprocess
