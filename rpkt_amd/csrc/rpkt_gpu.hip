@@ -44,6 +44,7 @@ constexpr int kWinChunks = kWin / 16;
 constexpr int kSlot = kWin + 4;      // LDS slot stride: 33 dwords, so lane-strided
                                      // reads of the 64 slots hit 32 distinct banks
 constexpr int kStreamUnroll = 4;     // 16-B chunk loads in flight per lane per step
+constexpr int kChainStreamUnroll = 8;  // the same in the mbuf-chain kernel
 constexpr uint64_t kMaxFrameBytes = 0xffffff00ull;  // voffset + 16 never wraps
 constexpr uint32_t kSplitStreamBytes = 65536;  // tile stream above which edge lines go first
 
@@ -188,9 +189,10 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 d, int lo, int hi) {
 // offset: zeros, no traffic), so the vmcnt waits stay exact.  A full chunk ends at or
 // before its range end, so it never straddles the end of the buffer; only an edge
 // chunk can, and it is re-read exactly after the loop.  `oob` = the descriptor's range.
+template <int U>
 struct StreamBatch {
-    u32x4 d[kStreamUnroll];
-    uint32_t m[kStreamUnroll];       // owner q | first << 8 | last << 9
+    u32x4 d[U];
+    uint32_t m[U];                   // owner q | first << 8 | last << 9
 };
 
 // Per-lane cursor over the concatenated full chunks: the owner range q of the lane's
@@ -206,12 +208,12 @@ __device__ __forceinline__ void cursor_load(const WaveScratch& W, StreamCursor& 
     k.off = W.s[q];
 }
 
-template <int AUX>
+template <int AUX, int U>
 __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
                                              const WaveScratch& W, uint32_t total, uint32_t base,
-                                             int lane, StreamCursor& k, StreamBatch& B) {
+                                             int lane, StreamCursor& k, StreamBatch<U>& B) {
 #pragma unroll
-    for (int u = 0; u < kStreamUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
         const uint32_t c = base + u * kWave + lane;
         const bool valid = c < total;
         if (valid && k.p1 <= c) {
@@ -230,10 +232,11 @@ __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t
     }
 }
 
+template <int U>
 __device__ __forceinline__ void stream_consume(WaveScratch& W, uint32_t& run,
-                                               const StreamBatch& B) {
+                                               const StreamBatch<U>& B) {
 #pragma unroll
-    for (int u = 0; u < kStreamUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
         const u32x4 d = B.d[u];
         const uint32_t v = hsum(d.w, hsum(d.z, hsum(d.y, hsum(d.x, 0u))));
         const uint32_t sc = wave_incl_scan(v) + run;
@@ -244,7 +247,7 @@ __device__ __forceinline__ void stream_consume(WaveScratch& W, uint32_t& run,
     }
 }
 
-template <int AUX = 0>
+template <int AUX = 0, int U = kStreamUnroll>
 __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
                                                     uint32_t s_abs, uint32_t e_abs,
                                                     WaveScratch& W, int lane) {
@@ -291,19 +294,19 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
     W.last[lane] = 0;
     wave_sync();
 
-    constexpr uint32_t kBatch = kWave * kStreamUnroll;
+    constexpr uint32_t kBatch = kWave * U;
     uint32_t run = 0;
     StreamCursor k;
     cursor_load(W, k, 0);
-    StreamBatch A, B;
+    StreamBatch<U> A, B;
     uint32_t base = 0;
-    stream_issue<AUX>(rs, oob, W, total, base, lane, k, A);
+    stream_issue<AUX, U>(rs, oob, W, total, base, lane, k, A);
     const uint32_t edge = edges();
     for (;;) {
-        stream_issue<AUX>(rs, oob, W, total, base + kBatch, lane, k, B);
-        stream_consume(W, run, A);
-        stream_issue<AUX>(rs, oob, W, total, base + 2 * kBatch, lane, k, A);
-        stream_consume(W, run, B);
+        stream_issue<AUX, U>(rs, oob, W, total, base + kBatch, lane, k, B);
+        stream_consume<U>(W, run, A);
+        stream_issue<AUX, U>(rs, oob, W, total, base + 2 * kBatch, lane, k, A);
+        stream_consume<U>(W, run, B);
         base += 2 * kBatch;
         if (base >= total) break;
     }
@@ -1105,7 +1108,7 @@ __device__ __forceinline__ uint32_t chain_stream(WaveScratch& W, __amdgpu_buffer
         const uint32_t last = v && (lane == kWave - 1 || t + 1 == cb[q + 1] - bq);
         citem[lane] = q | (swap << 8) | (last << 9) | ((uint32_t)v << 10);   // kept in LDS
         citem[kWave + lane] = he;                                               // over the stream
-        const uint32_t part = wave_stream_sum<2>(rs, fb, s_abs, e_abs, W, lane);
+        const uint32_t part = wave_stream_sum<2, kChainStreamUnroll>(rs, fb, s_abs, e_abs, W, lane);
         const uint32_t it = citem[lane];
         const uint32_t qq = it & 63u;
         if (it & (1u << 10)) {
@@ -1119,7 +1122,10 @@ __device__ __forceinline__ uint32_t chain_stream(WaveScratch& W, __amdgpu_buffer
 }
 
 template <bool L4>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+// A long chain makes a wave's item stream long and the grid small (256K 8000-B
+// chains = 4096 waves, one per SIMD): the stream keeps kChainStreamUnroll loads per
+// lane per batch in flight, and registers, not waves, are the budget (<= 256).
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 2)
 void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
                          const uint2* __restrict__ segs, uint32_t n_segs,
                          const uint32_t* __restrict__ chain_first, uint32_t n, uint32_t flags,
