@@ -2219,9 +2219,15 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             err_g = (uint32_t)g;
             break;
         }
-        // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl
-        o[4 + nl / 4] |= (uint32_t)p << (8 * (nl & 3));
-        o[8 + nl / 2] |= s << (16 * (nl & 1));
+        // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl (predicated: nl differs
+        // per lane, and a runtime register index would be a branch per register)
+        {
+            const uint32_t pw = (uint32_t)p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (nl >> 2) == k ? pw : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (nl >> 1) == k ? sw : 0u;
+        }
         nl += 1;
         e = end;
         s += hl;
