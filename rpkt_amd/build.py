@@ -16,8 +16,11 @@ ARCH = os.environ.get("RPKT_OFFLOAD_ARCH", "gfx950")
 
 GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
-GPU_SRC = [os.path.join(HERE, "csrc", "rpkt_gpu.hip")]
-GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_proto_table.h")]     # generated, included
+# the engine: one translation unit per kernel family, shared device code in rpkt_common.h
+GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
+           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_abi.hip")]
+GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
+            os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
 HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 
@@ -40,12 +43,18 @@ def source_hash():
 
 
 def build_gpu(force=False, extra=()):
+    """Compile the units in parallel (hipcc -c, gfx950), then link the shared library."""
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OUT, exist_ok=True)
-    if force or _stale(GPU_LIB, GPU_SRC + GPU_DEPS + HDR):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", '-DRPKT_SRC_HASH="%s"' % source_hash(), "-o", GPU_LIB] + \
-            list(extra) + GPU_SRC
-        subprocess.check_call(cmd)
+    if not (force or _stale(GPU_LIB, GPU_SRC + GPU_DEPS + HDR)):
+        return GPU_LIB
+    flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
+             '-DRPKT_SRC_HASH="%s"' % source_hash()] + list(extra)
+    objs = [os.path.join(OUT, os.path.basename(f).replace(".hip", ".o")) for f in GPU_SRC]
+    with ThreadPoolExecutor(max_workers=len(GPU_SRC)) as ex:
+        list(ex.map(lambda so: subprocess.check_call(flags + ["-c", "-o", so[1], so[0]]),
+                    zip(GPU_SRC, objs)))
+    subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", GPU_LIB] + objs)
     return GPU_LIB
 
 

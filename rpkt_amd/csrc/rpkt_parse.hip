@@ -1,0 +1,935 @@
+// rpkt_parse.hip — receive side: parse_kernel (frame batches), parse_chains_kernel
+// (mbuf chains), the flow-counter histogram and reduce, batched checksum::from_slice /
+// from_buf, and the streaming references tools/ablate.py times against the parse.
+#include "rpkt_common.h"
+
+namespace {
+
+// One wavefront per 64-frame tile: window loads -> LDS, lane-per-frame parse,
+// flattened L4 stream, LDS-staged coalesced record stores.  (A persistent variant
+// that prefetched the next tile's window into registers measured 1-3 % slower on
+// every config: the extra live registers cost more occupancy than the overlap gave.)
+// L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
+// tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
+// 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
+// 22 = default-policy stream loads, 23 = edge lines streamed first after the parse,
+// 24 = never, 25 = after the parse on long tiles).
+template <bool L4, int V>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
+void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                  const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                  uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
+                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+    const SpanSrc spans{offsets, stride, frame_len, frames_bytes, n};
+
+    // 1. header windows -> LDS (then, on long tiles, the edge lines: edge_lines_first)
+    const Frame fr = spans.get(i);
+    const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue<(V == 21) ? 2 : 0>(rs, frames_bytes, fr, lane, d, addr);
+        window_commit(W, rs, frames_bytes, d, addr, fix, lane);
+    }
+    EdgeLines X{false, 0u, 0u, 0u};
+    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25)
+        X = edge_lines_first(rs, frames_bytes, W, lane, valid, wend, fend);
+    wave_sync();
+
+    // 2. lane-per-frame parse
+    LaneRec L;
+    if constexpr (V == 1) {                                       // ablation: window only
+        const uint32_t* ww = reinterpret_cast<const uint32_t*>(&W.win[lane * kSlot]);
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < kWin / 4; ++k) x ^= ww[k];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) L.w[k] = x + k;
+        L.status = 0;
+    } else {
+        parse_lane(W, lane, fr, valid, flags, L);
+    }
+    if constexpr (V != 3) stage_record(W, lane, L.w);
+
+    // 3. L4 bytes beyond the window: flattened chunk stream over the tile.  The stream
+    // is read once: non-temporal loads (measured -13 % at 1500 B); the header windows
+    // keep the default policy (nt there measured slower).
+    if (L4 && V != 1) {
+        constexpr int kAux = (V == 22) ? 0 : 2;
+        uint32_t sp;
+        const uint32_t ss = L.stream_s, se = L.stream_e;
+        if (V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes)) {
+            // ablation: the same split taken after the parse
+            const uint32_t h1 = min(se, (ss + 127u) & ~127u);
+            const uint32_t t0 = max(se & ~127u, h1);
+            sp = wave_stream_sum<0>(rs, frames_bytes, ss, h1, W, lane);
+            sp += wave_stream_sum<0>(rs, frames_bytes, t0, se, W, lane);
+            sp += wave_stream_sum<kAux>(rs, frames_bytes, h1, t0, W, lane);
+        } else {
+            sp = stream_rest<kAux>(X, rs, frames_bytes, ss, se, wend, fend, W, lane);
+        }
+        if constexpr (V == 3) {                                   // ablation: 4 B per frame
+            uint32_t x = sp;
+#pragma unroll
+            for (int k = 0; k < 20; ++k) x ^= L.w[k];
+            if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+            return;
+        }
+        if (L.want_l4) {
+            const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
+            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
+        }
+    }
+    if constexpr (V == 3) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 20; ++k) x ^= L.w[k];
+        if (valid) reinterpret_cast<uint32_t*>(recs)[i] = x;
+        return;
+    }
+
+    // 4. records (+ flow events)
+    if ((flags & RPKT_F_FLOW_EV) && valid) {
+        const uint64_t ev = flow_event(L, rec_stage(W) + lane * 21, n_buckets);
+        __builtin_nontemporal_store(ev, &flow_ev[i]);
+    }
+    flush_records<V != 8>(W, lane, recs, p0, n);
+}
+
+// ---- mbuf chains: the same parse over rpkt-dpdk's Pbuf ----
+// A chain is a list of (offset, data_len) segments of one arena.  Over a Pbuf the
+// generic views test header sizes against chunk(), the rest of the segment that holds
+// the header's first byte (pbuf.rs:48-57, 86-96), and totals against remaining()
+// (pbuf.rs:98-101); trim_off cuts the packet end (pbuf.rs:117-140).  Segment 0 is
+// windowed into LDS like a frame, so every header that starts inside it is parsed by
+// the window path; a header that starts exactly at segment 0's end (the only way
+// past it) is read from global memory byte-wise on a rare path.  The L4 bytes past
+// the window are summed by the flattened chunk stream over (chain, segment) items,
+// each item's sum brought to segment 0's byte phase before it is added.
+struct ChainSrc {
+    const uint2* segs;
+    uint32_t fb;
+    __device__ __forceinline__ Frame seg(uint32_t k) const {
+        const uint2 v = segs[k];
+        const uint32_t off = v.x < fb ? v.x : fb;
+        const uint32_t len = v.y < fb - off ? v.y : fb - off;
+        return Frame{off, len};
+    }
+};
+
+// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout)
+__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t (&F)[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        F[k] = gbyte(rs, a + 4 * k) | (gbyte(rs, a + 4 * k + 1) << 8) |
+               (gbyte(rs, a + 4 * k + 2) << 16) | (gbyte(rs, a + 4 * k + 3) << 24);
+}
+// checksum::from_slice over n bytes at absolute `a` (rpkt/src/checksum.rs:33-62)
+__device__ __forceinline__ uint32_t gsum_be(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t n) {
+    uint32_t acc = 0, k = 0;
+    for (; k + 1 < n; k += 2) acc += (gbyte(rs, a + k) << 8) | gbyte(rs, a + k + 1);
+    if (k < n) acc += gbyte(rs, a + k) << 8;
+    return fold16(acc);
+}
+
+// Chunk at logical cursor c > 0 of segments [a, b) under the packet end `limit`: the
+// rest of the first segment whose end passes c (empty segments skipped, as
+// advance_common walks), cut at limit.  `abs` = the chunk's first byte.
+__device__ __forceinline__ uint32_t chain_chunk(const ChainSrc& S, uint32_t a, uint32_t b,
+                                                uint32_t c, uint32_t limit, uint32_t& abs) {
+    uint32_t cum = 0;
+    for (uint32_t k = a; k < b; ++k) {
+        const Frame s = S.seg(k);
+        const uint32_t end = cum + s.len;
+        if (end > c) {
+            abs = s.off + (c - cum);
+            return (end < limit ? end : limit) - c;
+        }
+        cum = end;
+    }
+    abs = S.fb;
+    return 0;
+}
+
+// Lane-per-chain parse: parse_lane with the chunk/remaining distinction of a Pbuf.
+// C = segment 0's length: headers starting below C are read from the LDS window.
+__device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane, Frame s0,
+                                                 uint32_t pkt, const ChainSrc& S, uint32_t a,
+                                                 uint32_t b, __amdgpu_buffer_rsrc_t rs,
+                                                 uint32_t flags, LaneRec& L) {
+    const uint32_t ph = s0.off & 15u;
+    const uint8_t* slot = &W.win[lane * kSlot];
+    uint32_t* w = L.w;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = 0;
+    const uint32_t C = s0.len;                                 // Pbuf::new, pbuf.rs:19-34
+    L.stream_s = L.stream_e = L.l4_part = L.l4_start_abs = L.pseudo = 0;
+    L.want_l4 = false;
+    w[19] = pkt;
+    uint32_t status = RPKT_S_OK;
+
+    uint32_t E[6];
+    {
+        const uint32_t a0 = ph & ~3u, sh = ph & 3u;
+        uint32_t R[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) R[k] = lds32(slot, a0 + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) E[k] = align_bytes(R[k + 1], R[k], sh);
+    }
+    if (C < 14) {                                              // ether/generated.rs:36
+        L.status = RPKT_S_ETH_SHORT;
+        w[0] = RPKT_S_ETH_SHORT;
+        return;
+    }
+    w[1] = E[0];
+    w[2] = E[1];
+    w[3] = E[2];
+    const uint32_t eth_et = be16_lo(E[3]);
+    uint32_t nvlan = 0, et = eth_et, c = 14;
+#pragma unroll
+    for (int v = 0; v < RPKT_MAX_VLAN; ++v) {                  // vlan/generated.rs:32-61
+        if (!is_tag(et)) break;
+        uint32_t T = 0, ck = 0;
+        if (c < C) {
+            ck = C - c;
+            T = v == 0 ? align_bytes(E[4], E[3], 2) : align_bytes(E[5], E[4], 2);
+        } else if (c < pkt) {
+            uint32_t ab;
+            ck = chain_chunk(S, a, b, c, pkt, ab);
+            T = gbyte(rs, ab) | (gbyte(rs, ab + 1) << 8) | (gbyte(rs, ab + 2) << 16) |
+                (gbyte(rs, ab + 3) << 24);
+        }
+        if (ck < 4) {
+            status = RPKT_S_VLAN_SHORT;
+            break;
+        }
+        et = be16_hi(T);
+        w[4] |= be16_lo(T) << (16 * v);
+        w[5] |= et << (16 * v);
+        nvlan += 1;
+        c += 4;
+    }
+    w[0] = (nvlan << 8) | (eth_et << 16);
+    if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+
+    // Ipv4::parse (ipv4/generated.rs:35-51): chunk vs remaining
+    const uint32_t l3 = c;
+    w[16] = l3;
+    Hdr6 ip;
+    uint32_t ck3 = 0, ab3 = 0;
+    const bool fast3 = l3 < C;
+    if (fast3) {
+        ck3 = C - l3;
+        read_hdr(slot, ph + l3, ip);
+    } else {
+        if (l3 < pkt) ck3 = chain_chunk(S, a, b, l3, pkt, ab3);
+        gread20(rs, ck3 ? ab3 : S.fb, ip.F);
+    }
+    const uint32_t vhl = ip.F[0] & 0xffu;
+    const uint32_t ihl4 = (vhl & 0xfu) * 4u;
+    const uint32_t tot = be16_hi(ip.F[0]);
+    if (ck3 < 20) status = RPKT_S_IP_SHORT;
+    else if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
+    else if (ihl4 > ck3) status = RPKT_S_IP_IHL_GT_LEN;
+    else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
+    else if (tot > pkt - l3) status = RPKT_S_IP_TOT_GT_LEN;
+    if (status != RPKT_S_OK) {
+        w[0] |= status;
+        L.status = status;
+        return;
+    }
+    const uint32_t proto = (ip.F[2] >> 8) & 0xffu;
+    const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
+    w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
+    w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
+    w[8] = (ip.F[2] & 0xffffu) | (be16_hi(ip.F[2]) << 16);
+    w[9] = src;
+    w[10] = dst;
+    if (flags & RPKT_F_IP_SUM)
+        w[18] = fast3 ? be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4),
+                               s0.off + l3)
+                      : gsum_be(rs, ab3, ihl4);
+    const uint32_t l4 = l3 + ihl4, limit = l3 + tot;           // Ipv4::payload :115-127
+    const uint32_t l4rem = tot - ihl4;
+    w[16] |= l4 << 16;
+    w[17] = l4 | (l4rem << 16);
+
+    // Udp::parse / Tcp::parse against the chunk at l4 under the trimmed end
+    Hdr6 h4;
+    uint32_t ck4 = 0, ab4 = 0;
+    const bool fast4 = l4 < C;
+    if (fast4) {
+        ck4 = (C < limit ? C : limit) - l4;
+        read_hdr(slot, ph + l4, h4);
+    } else {
+        if (l4 < limit) ck4 = chain_chunk(S, a, b, l4, limit, ab4);
+        gread20(rs, ck4 ? ab4 : S.fb, h4.F);
+    }
+    uint32_t l4len = 0;
+    if (proto == 17u) {
+        const uint32_t ulen = be16_lo(h4.F[1]);
+        if (ck4 < 8) status = RPKT_S_UDP_SHORT;
+        else if (ulen < 8 || ulen > l4rem) status = RPKT_S_UDP_BAD_LEN;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[14] = ulen;
+            w[15] = be16_hi(h4.F[1]);
+            w[17] = (l4 + 8) | ((ulen - 8) << 16);
+            l4len = ulen;
+        }
+    } else if (proto == 6u) {
+        const uint32_t hl = ((h4.F[3] >> 4) & 0xfu) * 4u;
+        if (ck4 < 20) status = RPKT_S_TCP_SHORT;
+        else if (hl < 20 || hl > ck4) status = RPKT_S_TCP_BAD_DOFF;
+        else {
+            w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
+            w[12] = bswap32(h4.F[1]);
+            w[13] = bswap32(h4.F[2]);
+            w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
+            w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
+            w[17] = (l4 + hl) | ((l4rem - hl) << 16);
+            l4len = l4rem;
+        }
+    } else {
+        status = RPKT_S_L4_OTHER;
+    }
+    w[0] |= status;
+    L.status = status;
+    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+        L.want_l4 = true;
+        L.pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto + l4len;
+        const uint32_t e = l4 + l4len;
+        L.l4_start_abs = s0.off + l4;                          // segment 0's byte phase
+        if (fast4) {
+            const uint32_t win_end = kWin - ph;
+            uint32_t e_in = e < win_end ? e : win_end;
+            e_in = e_in < C ? e_in : C;
+            L.l4_part = raw_range_sum(slot, h4.R, h4.a0, ph + l4, ph + e_in);
+            L.stream_s = e_in;
+        } else {
+            L.stream_s = l4;
+        }
+        L.stream_e = e;                                        // logical, not absolute
+    }
+}
+
+// Sum of the logical range [ss, se) of this lane's chain, in segment 0's byte phase,
+// for every lane of the wave.  Items (chain, segment intersecting its range) are
+// flattened in chain order; each round streams 64 of them with wave_stream_sum.
+// An item's logical start is its owner's running cursor plus a segmented prefix sum
+// of the round's segment lengths.  Scratch: the window area past the staged records
+// (dwords [0, 513) of it; the caller keeps per-lane values at [513, 705)).
+__device__ __forceinline__ uint32_t chain_stream(WaveScratch& W, __amdgpu_buffer_rsrc_t rs,
+                                                 uint32_t fb, const ChainSrc& S, uint32_t a,
+                                                 uint32_t b, uint32_t off0, uint32_t ss,
+                                                 uint32_t se, int lane) {
+    uint32_t k = 0, fi = 0, ls0 = 0;
+    if (se > ss) {
+        uint32_t cum = 0;
+        for (uint32_t j = a; j < b; ++j) {
+            const uint32_t len = S.seg(j).len;
+            if (cum + len > ss && cum < se) {
+                if (k == 0) {
+                    fi = j;
+                    ls0 = cum;
+                }
+                ++k;
+            }
+            cum += len;
+            if (cum >= se) break;
+        }
+    }
+    const uint32_t incl = wave_incl_scan(k);
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    if (T == 0) return 0;                                      // wave-uniform
+    uint32_t* X = rec_stage(W) + kWave * 21;
+    uint32_t* cb = X;                  // [65] first item of each lane
+    uint32_t* cfi = X + 65;            // first segment index
+    uint32_t* ccum = X + 129;          // logical start of the lane's next item
+    uint32_t* css = X + 193;
+    uint32_t* cse = X + 257;
+    uint32_t* cacc = X + 321;
+    uint32_t* citem = X + 385;         // [128] per-item state held over the stream
+    cb[lane] = incl - k;
+    if (lane == 63) cb[64] = incl;
+    cfi[lane] = fi | (off0 << 31);     // segment 0's byte parity in bit 31
+    ccum[lane] = ls0;
+    css[lane] = ss;
+    cse[lane] = se;
+    cacc[lane] = 0;
+    wave_sync();
+    for (uint32_t r0 = 0; r0 < T; r0 += kWave) {
+        const uint32_t g = r0 + lane;
+        const bool v = g < T;
+        uint32_t q = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (cb[q + step] <= g) q += step;
+        const uint32_t bq = cb[q];
+        const uint32_t t = g - bq;
+        const uint32_t fq = cfi[q];
+        const Frame sg = v ? S.seg((fq & 0x7fffffffu) + t) : Frame{0, 0};
+        const uint32_t x = sg.len;
+        const uint32_t inc = wave_incl_scan(x);
+        const uint32_t j0 = (bq > r0 ? bq : r0) - r0;          // owner's first lane this round
+        const uint32_t base = (uint32_t)__shfl((int)(inc - x), (int)j0, kWave);
+        const uint32_t ls = ccum[q] + (inc - x) - base;
+        const uint32_t lo = ls > css[q] ? ls : css[q];
+        const uint32_t he = ls + x, hi = he < cse[q] ? he : cse[q];
+        uint32_t s_abs = 0, e_abs = 0;
+        if (v && hi > lo) {
+            s_abs = sg.off + (lo - ls);
+            e_abs = sg.off + (hi - ls);
+        }
+        const uint32_t swap = ((sg.off - ls) ^ (fq >> 31)) & 1u;
+        const uint32_t last = v && (lane == kWave - 1 || t + 1 == cb[q + 1] - bq);
+        citem[lane] = q | (swap << 8) | (last << 9) | ((uint32_t)v << 10);   // kept in LDS
+        citem[kWave + lane] = he;                                               // over the stream
+        const uint32_t part = wave_stream_sum<2, kChainStreamUnroll>(rs, fb, s_abs, e_abs, W, lane);
+        const uint32_t it = citem[lane];
+        const uint32_t qq = it & 63u;
+        if (it & (1u << 10)) {
+            uint32_t c = fold16(part);
+            atomicAdd(&cacc[qq], (it & (1u << 8)) ? bswap16(c) : c);
+        }
+        if (it & (1u << 9)) ccum[qq] = citem[kWave + lane];
+        wave_sync();
+    }
+    return cacc[lane];
+}
+
+template <bool L4>
+// A long chain makes a wave's item stream long and the grid small (256K 8000-B
+// chains = 4096 waves, one per SIMD): the stream keeps kChainStreamUnroll loads per
+// lane per batch in flight, and registers, not waves, are the budget (<= 256).
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 2)
+void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
+                         const uint2* __restrict__ segs, uint32_t n_segs,
+                         const uint32_t* __restrict__ chain_first, uint32_t n, uint32_t flags,
+                         rpkt_rec_t* __restrict__ recs, uint64_t* __restrict__ flow_ev,
+                         uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(buf, fb);
+    const ChainSrc S{segs, fb};
+
+    // chain bounds, segment 0 and pkt_len (sum of data_len, saturating)
+    uint32_t a = 0, b = 0;
+    if (valid) {
+        const uint32_t f0 = chain_first[i], f1 = chain_first[i + 1];
+        a = f0 < n_segs ? f0 : n_segs;
+        b = f1 > a ? f1 : a;
+        b = b < n_segs ? b : n_segs;
+    }
+    Frame s0{0, 0};
+    uint32_t pkt = 0;
+    for (uint32_t k = a; k < b; ++k) {
+        const Frame s = S.seg(k);
+        if (k == a) s0 = s;
+        pkt = pkt + s.len < pkt ? 0xffffffffu : pkt + s.len;
+    }
+
+    // 1. segment 0's header window -> LDS
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, s0, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    wave_sync();
+
+    // 2. lane-per-chain parse
+    LaneRec L;
+    parse_chain_lane(W, lane, s0, pkt, S, a, b, rs, flags, L);
+    stage_record(W, lane, L.w);
+
+    // 3. L4 bytes past the window, across segments (the in-window part and the
+    //    pseudo header wait in LDS, past chain_stream's scratch)
+    if (L4) {
+        uint32_t* keep = rec_stage(W) + kWave * 21 + 513;
+        keep[lane] = L.l4_part;
+        keep[kWave + lane] = L.want_l4 ? (L.pseudo | 0x80000000u) : 0u;
+        keep[2 * kWave + lane] = L.l4_start_abs;
+        const uint32_t acc = chain_stream(W, rs, fb, S, a, b, s0.off, L.stream_s, L.stream_e, lane);
+        const uint32_t ps = keep[kWave + lane];
+        if (ps) {
+            const uint32_t sum = be_sum(keep[lane] + acc, keep[2 * kWave + lane]);
+            rec_stage(W)[lane * 21 + 18] |= fold16((ps & 0x7fffffffu) + sum) << 16;
+        }
+    }
+
+    // 4. records (+ flow events)
+    if ((flags & RPKT_F_FLOW_EV) && valid) {
+        const uint64_t ev = flow_event(L, rec_stage(W) + lane * 21, n_buckets);
+        __builtin_nontemporal_store(ev, &flow_ev[i]);
+    }
+    flush_records<true>(W, lane, recs, p0, n);
+}
+
+// Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
+// chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
+template <int U, bool NT>
+__global__ __launch_bounds__(256)
+void copy_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, u32x4* __restrict__ out,
+                     uint32_t out16) {
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t i = t;
+    for (; i + (U - 1) * T < in16; i += U * T) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = in[i + u * T];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= x[u];
+    }
+    for (; i < in16; i += T) acc ^= in[i];
+    for (uint32_t j = t; j < out16; j += T) {
+        if constexpr (NT) __builtin_nontemporal_store(acc + j, &out[j]);
+        else out[j] = acc + j;
+    }
+}
+
+// Read-only streaming reference (what HBM gives a pure 16-B/lane read stream).
+__global__ __launch_bounds__(256)
+void read_ref_kernel(const u32x4* __restrict__ in, uint32_t in16, uint32_t* __restrict__ out) {
+    const uint32_t T = gridDim.x * blockDim.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t i = t;
+    for (; i + 7 * T < in16; i += 8 * T) {
+        u32x4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = in[i + u * T];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u];
+    }
+    for (; i < in16; i += T) acc ^= in[i];
+    const uint32_t r = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (r == 0x12345678u) out[t] = r;       // keeps the loads live, never taken in practice
+}
+
+// Same-traffic reference for the parse: each wave reads its 64-frame tile's bytes as
+// one contiguous non-temporal 16-B/lane stream and writes 64 records (80 B each) with
+// non-temporal stores, like parse_kernel, but does no parse work.  `tile_bytes` is the
+// tile's span (64 x stride); the last tile is clipped.
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                        const uint32_t* __restrict__ offsets, uint32_t tile_bytes, uint32_t n,
+                        u32x4* __restrict__ out) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t t = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const uint32_t p0 = t * kWave;
+    if (p0 >= n) return;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+    uint32_t s = t * tile_bytes, e = s + tile_bytes;
+    if (offsets) {                                   // packed: the tile's frames' span
+        s = offsets[p0];
+        e = offsets[p0 + kWave < n ? p0 + kWave : n];
+    }
+    e = e < frames_bytes ? e : frames_bytes;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    for (uint32_t a = (s & ~15u) + 16u * lane; a < e; a += 16u * kWave * 8) {
+        u32x4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = load16_fast<2>(rs, a + 16u * kWave * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= x[u];
+    }
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane;
+        if (c / 5 < nrec) __builtin_nontemporal_store(acc + c, &out[(size_t)p0 * 5 + c]);
+    }
+}
+
+// ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
+// One workgroup per CU-sized slice of the events; each keeps {pkts, bytes,
+// ip_bad | l4_bad << 16} per bucket in LDS (u32; a slice holds < 65536 events,
+// so no field can overflow), writes it once to its slab, and a second kernel
+// sums the slabs in a fixed order (bitwise reproducible counters).
+constexpr int kFlowThreads = 512;
+constexpr uint32_t kFlowLdsMax = 8192;      // buckets (+1 unparsed row) privatised in LDS
+constexpr uint32_t kFlowMaxPerBlock = 32768;
+constexpr uint32_t kFlowMinBlocks = 256;
+constexpr int kFlowUnroll = 8;
+
+__host__ __device__ inline uint32_t flow_blocks(uint32_t n) {
+    uint32_t b = (n + kFlowMaxPerBlock - 1) / kFlowMaxPerBlock;
+    uint32_t m = (n + kFlowThreads - 1) / kFlowThreads;   // >= one event per thread
+    uint32_t want = kFlowMinBlocks < m ? kFlowMinBlocks : m;
+    return b > want ? b : (want ? want : 1);
+}
+
+__global__ __launch_bounds__(kFlowThreads)
+void flow_hist_kernel(const uint64_t* __restrict__ ev, uint32_t n, uint32_t per_block,
+                      uint32_t n_buckets, uint32_t* __restrict__ slab) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t h[];   // 3 * (n_buckets + 1)
+    const uint32_t rows = n_buckets + 1;
+    for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) h[r] = 0;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * per_block;
+    const uint32_t hi = min(n, lo + per_block);
+    for (uint32_t i0 = lo; i0 < hi; i0 += kFlowThreads * kFlowUnroll) {
+        uint64_t e[kFlowUnroll];
+#pragma unroll
+        for (int u = 0; u < kFlowUnroll; ++u) {
+            const uint32_t i = i0 + u * kFlowThreads + threadIdx.x;
+            e[u] = i < hi ? ev[i] : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kFlowUnroll; ++u) {
+            if (e[u] == ~0ull) continue;
+            uint32_t b = (uint32_t)(e[u] >> 32) & 0xffffu;
+            if (b > n_buckets) b = n_buckets;
+            atomicAdd(&h[b], 1u);
+            atomicAdd(&h[rows + b], (uint32_t)e[u]);
+            const uint32_t bad =
+                (uint32_t)((e[u] >> 48) & 1u) | ((uint32_t)((e[u] >> 49) & 1u) << 16);
+            if (bad) atomicAdd(&h[2 * rows + b], bad);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = slab + (size_t)blockIdx.x * 3 * rows;
+    for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) out[r] = h[r];
+}
+
+// Slab reduce without atomics: block x owns buckets [64x, 64x + 64); its 16 waves
+// split the slabs (wave w sums slabs w, w + 16, ...; lane = bucket, so every load is
+// a coalesced 256-B row), the 16 partials meet in LDS, and wave 0 adds the totals to
+// the counters.  Each bucket has one writer, and integer sums in a fixed order give
+// the same bits every run.  (The earlier form, 16 slab groups per bucket joined by
+// u64 atomics, was atomic-bound: 18 us at 8M events; 4 groups 35 us, 64 groups 38 us.)
+constexpr uint32_t kReduceWaves = 16;
+
+__global__ __launch_bounds__(kWave * kReduceWaves)
+void flow_reduce_kernel(const uint32_t* __restrict__ slab, uint32_t n_slabs,
+                        uint32_t n_buckets, unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t part[kReduceWaves][5][kWave];     // pk, bytes lo, bytes hi, ipb, l4b
+    const uint32_t rows = n_buckets + 1;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint32_t b = blockIdx.x * kWave + lane;
+    uint32_t pk = 0, ipb = 0, l4b = 0;
+    uint64_t by = 0;
+    if (b < rows) {
+#pragma unroll 4
+        for (uint32_t s = w; s < n_slabs; s += kReduceWaves) {
+            const uint32_t* sl = slab + (size_t)s * 3 * rows;
+            pk += sl[b];
+            by += sl[rows + b];
+            const uint32_t bad = sl[2 * rows + b];
+            ipb += bad & 0xffffu;
+            l4b += bad >> 16;
+        }
+    }
+    part[w][0][lane] = pk;
+    part[w][1][lane] = (uint32_t)by;
+    part[w][2][lane] = (uint32_t)(by >> 32);
+    part[w][3][lane] = ipb;
+    part[w][4][lane] = l4b;
+    __syncthreads();
+    if (w != 0 || b >= rows) return;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kReduceWaves; ++k) {
+        t0 += part[k][0][lane];
+        t1 += part[k][1][lane] | ((uint64_t)part[k][2][lane] << 32);
+        t2 += part[k][3][lane];
+        t3 += part[k][4][lane];
+    }
+    counters[4 * b + 0] += t0;
+    counters[4 * b + 1] += t1;
+    counters[4 * b + 2] += t2;
+    counters[4 * b + 3] += t3;
+}
+
+// n_buckets above the LDS limit: one global atomic set per event.
+__global__ void flow_atomic_kernel(const uint64_t* __restrict__ ev, uint32_t n,
+                                   uint32_t n_buckets, unsigned long long* counters) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t e = ev[i];
+        uint32_t b = (uint32_t)(e >> 32) & 0xffffu;
+        if (b > n_buckets) b = n_buckets;
+        atomicAdd(&counters[4 * b + 0], 1ull);
+        atomicAdd(&counters[4 * b + 1], (unsigned long long)(e & 0xffffffffu));
+        if ((e >> 48) & 1u) atomicAdd(&counters[4 * b + 2], 1ull);
+        if ((e >> 49) & 1u) atomicAdd(&counters[4 * b + 3], 1ull);
+    }
+}
+
+// ---- batched checksum::from_slice over ranges ----
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void checksum_ranges_kernel(const uint8_t* __restrict__ buf, uint32_t buf_bytes,
+                            const uint32_t* __restrict__ ranges, uint32_t n,
+                            uint16_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    uint32_t s = 0, e = 0;
+    if (i < n) {
+        uint64_t st = ranges[2 * i], ln = ranges[2 * i + 1];
+        if (st > buf_bytes) st = buf_bytes;
+        if (st + ln > buf_bytes) ln = buf_bytes - st;
+        s = (uint32_t)st;
+        e = (uint32_t)(st + ln);
+    }
+    const uint32_t part =
+        wave_stream_sum(make_rsrc(buf, buf_bytes), buf_bytes, s, e, scratch[wid], lane);
+    if (i < n) out[i] = (uint16_t)be_sum(part, s);
+}
+
+// ---- batched checksum::from_buf over segment chains (mbuf chains) ----
+// Pass 1: every segment's standalone big-endian sum (the ranges kernel) plus its
+// length parity.  Pass 2: lane per chain folds its segments in order; a segment that
+// starts at an odd offset of the chain's byte stream contributes its byte-swapped
+// sum, which is exactly from_buf's pairing of a chunk's odd tail byte with the next
+// chunk's first byte (checksum.rs:13-24, 82-88).
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void segment_sums_kernel(const uint8_t* __restrict__ buf, uint32_t buf_bytes,
+                         const uint32_t* __restrict__ segs, uint32_t n,
+                         uint32_t* __restrict__ seg_out) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    uint32_t s = 0, e = 0, len = 0;
+    if (i < n) {
+        uint64_t st = segs[2 * i], ln = segs[2 * i + 1];
+        len = (uint32_t)ln;
+        if (st > buf_bytes) st = buf_bytes;
+        if (st + ln > buf_bytes) ln = buf_bytes - st;
+        s = (uint32_t)st;
+        e = (uint32_t)(st + ln);
+    }
+    const uint32_t part =
+        wave_stream_sum(make_rsrc(buf, buf_bytes), buf_bytes, s, e, scratch[wid], lane);
+    if (i < n) seg_out[i] = be_sum(part, s) | ((len & 1u) << 16);
+}
+
+__global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
+                                  const uint32_t* __restrict__ first, uint32_t n_chains,
+                                  uint32_t n_segs, uint16_t* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_chains) return;
+    uint32_t a = first[p], b = first[p + 1];
+    if (b > n_segs) b = n_segs;
+    uint32_t acc = 0, odd = 0;
+    for (uint32_t i = a; i < b; ++i) {
+        const uint32_t v = seg_out[i];
+        const uint32_t sum = v & 0xffffu;
+        acc += odd ? bswap16(sum) : sum;
+        odd ^= v >> 16;
+    }
+    out[p] = (uint16_t)fold16(acc);
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_t dp,
+                        uint8_t proto) {
+    uint32_t h = 0x811c9dc5u;
+    h = (h ^ ip_src) * 0x01000193u;
+    h = (h ^ ip_dst) * 0x01000193u;
+    h = (h ^ (((uint32_t)sp << 16) | dp)) * 0x01000193u;
+    h = (h ^ proto) * 0x01000193u;
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+
+int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs_dev,
+                         rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0> : parse_kernel<false, 0>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+
+int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,
+                          rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!c || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (c->n_chains == 0) return RPKT_OK;
+    if (!c->chain_first_dev || (c->n_segs && (!c->buf_dev || !c->segs_dev))) return RPKT_E_INVAL;
+    if (c->buf_bytes > kMaxFrameBytes || c->n_segs >= 0x80000000u) return RPKT_E_TOO_LARGE;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)c->segs_dev & 7u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (c->n_chains + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_chains_kernel<true> : parse_chains_kernel<false>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, c->buf_dev,
+                  (uint32_t)c->buf_bytes, (const uint2*)c->segs_dev, c->n_segs,
+                  c->chain_first_dev, c->n_chains, flags, recs_dev, (uint64_t*)flow_ev_dev,
+                  n_buckets);
+}
+
+int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs, int variant,
+                           void* stream) {
+    if (!b || !recs || b->n == 0) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    hipStream_t st = (hipStream_t)stream;
+#define RPKT_V(v)                                                                       \
+    launch((flags & RPKT_F_L4_SUM) ? parse_kernel<true, v> : parse_kernel<false, v>,   \
+           dim3(grid), dim3(per_block), 0, st, b->frames_dev, (uint32_t)b->frames_bytes,   \
+           b->offsets_dev, b->stride, flen, b->n, flags, recs, (uint64_t*)nullptr, 0u)
+    switch (variant) {
+        case 0: return RPKT_V(0);
+        case 1: return RPKT_V(1);
+        case 3: return RPKT_V(3);
+        case 8: return RPKT_V(8);
+        case 21: return RPKT_V(21);
+        case 22: return RPKT_V(22);
+        case 23: return RPKT_V(23);
+        case 24: return RPKT_V(24);
+        case 25: return RPKT_V(25);
+        case 10:
+            return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 11:
+            return launch(copy_ref_kernel<8, false>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 12:
+            return launch(copy_ref_kernel<8, true>, dim3(2048), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        case 14:
+            return launch(read_ref_kernel, dim3(4096), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (uint32_t*)recs);
+        case 15:
+            return launch(tile_rw_ref_kernel, dim3(grid), dim3(per_block), 0, st, b->frames_dev,
+                          (uint32_t)b->frames_bytes, b->offsets_dev, b->stride * kWave, b->n,
+                          (u32x4*)recs);
+        case 13:
+            return launch(copy_ref_kernel<8, false>, dim3(8192), dim3(256), 0, st,
+                          (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
+                          (u32x4*)recs, b->n * (RPKT_REC_BYTES / 16));
+        default: return RPKT_E_INVAL;
+    }
+#undef RPKT_V
+}
+
+size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets) {
+    if (n_buckets > kFlowLdsMax) return 16;
+    return (size_t)flow_blocks(n) * 3 * (size_t)(n_buckets + 1) * sizeof(uint32_t);
+}
+
+int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets,
+                        uint64_t* counters, void* workspace, void* stream) {
+    if (!counters || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS) return RPKT_E_INVAL;
+    if (n == 0) return RPKT_OK;
+    if (!ev) return RPKT_E_INVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (n_buckets > kFlowLdsMax) {
+        return launch(flow_atomic_kernel, dim3(1024), dim3(256), 0, st, (const uint64_t*)ev, n,
+                      n_buckets, (unsigned long long*)counters);
+    }
+    if (!workspace) return RPKT_E_INVAL;
+    const uint32_t slabs = flow_blocks(n);
+    const uint32_t per = (n + slabs - 1) / slabs;
+    const size_t lds = 3 * (size_t)(n_buckets + 1) * sizeof(uint32_t);
+    static bool attr_set = false;
+    if (!attr_set) {
+        int rc0 = hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+        if (rc0) return rc0;
+        attr_set = true;
+    }
+    int rc = launch(flow_hist_kernel, dim3(slabs), dim3(kFlowThreads), lds, st,
+                    (const uint64_t*)ev, n, per, n_buckets, (uint32_t*)workspace);
+    if (rc) return rc;
+    const uint32_t rows = n_buckets + 1;
+    return launch(flow_reduce_kernel, dim3((rows + kWave - 1) / kWave), dim3(kWave * kReduceWaves),
+                  0, st, (const uint32_t*)workspace, slabs, n_buckets,
+                  (unsigned long long*)counters);
+}
+
+int rpkt_gpu_checksum_ranges(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* ranges,
+                             uint32_t n, uint16_t* out, void* stream) {
+    if (n == 0) return RPKT_OK;
+    if (!buf || !ranges || !out) return RPKT_E_INVAL;
+    if (buf_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    return launch(checksum_ranges_kernel, dim3((n + per_block - 1) / per_block), dim3(per_block),
+                  0, (hipStream_t)stream, buf, (uint32_t)buf_bytes, ranges, n, out);
+}
+
+size_t rpkt_gpu_checksum_chains_workspace_bytes(uint32_t n_segs) {
+    return (size_t)(n_segs ? n_segs : 1) * sizeof(uint32_t);
+}
+
+int rpkt_gpu_checksum_chains(const uint8_t* buf, uint64_t buf_bytes, const uint32_t* segs,
+                             uint32_t n_segs, const uint32_t* chain_first, uint32_t n_chains,
+                             uint16_t* out, void* workspace, void* stream) {
+    if (n_chains == 0) return RPKT_OK;
+    if (!chain_first || !out || (n_segs && (!buf || !segs || !workspace))) return RPKT_E_INVAL;
+    if (buf_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    if (n_segs) {
+        int rc = launch(segment_sums_kernel, dim3((n_segs + per_block - 1) / per_block),
+                        dim3(per_block), 0, st, buf, (uint32_t)buf_bytes, segs, n_segs,
+                        (uint32_t*)workspace);
+        if (rc) return rc;
+    }
+    return launch(chain_fold_kernel, dim3((n_chains + 255) / 256), dim3(256), 0, st,
+                  (const uint32_t*)workspace, chain_first, n_chains, n_segs, out);
+}
+
+}  // extern "C"

@@ -1,0 +1,431 @@
+// rpkt_tx.hip — transmit side: build_kernel (prepend_header + setters + checksum fill)
+// and forward_kernel (the loopback_rx firewall loop fused into one pass).
+#include "rpkt_common.h"
+
+namespace {
+
+// ---- TX side: header build and the loopback_rx forward rewrite ----
+// Both compose the fixed header bytes of a frame from an rpkt_rec_t in the frame's
+// LDS slot (slot byte x <-> absolute (off & ~15) + x, as for the parse window) and
+// write them back with wave-cooperative 16-B chunk stores: a chunk wholly inside a
+// frame's written ranges is one dwordx4 store, a partial one (at most the first and
+// last of each range) is stored byte by byte, so no byte outside the frame's own
+// header ranges is ever written (neighbouring frames are rewritten concurrently).
+__device__ __forceinline__ void put_be16(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+}
+__device__ __forceinline__ void put_be32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+
+// Fixed header bytes from record words (include/rpkt_gpu.h layout): Ethernet, n_vlan
+// tags, the 20 IPv4 bytes at l3, the UDP header or the 20 TCP bytes at l4.  These
+// are exactly the bytes prepend_header + setters write (ether/generated.rs:71-88,
+// vlan/generated.rs:73-100, ipv4/generated.rs:130-206, udp/generated.rs:79-104,
+// tcp/generated.rs:135-224); option bytes are not touched.
+__device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20], uint32_t nv,
+                                             uint32_t l3, uint32_t l4, uint32_t proto,
+                                             uint32_t ip_len, uint32_t udp_len, uint32_t ip_ck,
+                                             uint32_t l4_ck) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s[k] = (uint8_t)(w[1 + k / 4] >> (8 * (k % 4)));
+    put_be16(s + 12, w[0] >> 16);
+#pragma unroll
+    for (uint32_t v = 0; v < RPKT_MAX_VLAN; ++v) {
+        if (v < nv) {
+            put_be16(s + 14 + 4 * v, w[4] >> (16 * v));
+            put_be16(s + 16 + 4 * v, w[5] >> (16 * v));
+        }
+    }
+    uint8_t* ip = s + l3;
+    ip[0] = (uint8_t)w[6];
+    ip[1] = (uint8_t)(w[6] >> 8);
+    put_be16(ip + 2, ip_len);
+    put_be16(ip + 4, w[7]);
+    put_be16(ip + 6, w[7] >> 16);
+    ip[8] = (uint8_t)w[8];
+    ip[9] = (uint8_t)(w[8] >> 8);
+    put_be16(ip + 10, ip_ck);
+    put_be32(ip + 12, w[9]);
+    put_be32(ip + 16, w[10]);
+    uint8_t* t = s + l4;
+    if (proto == 17u) {
+        put_be16(t, w[11]);
+        put_be16(t + 2, w[11] >> 16);
+        put_be16(t + 4, udp_len);
+        put_be16(t + 6, l4_ck);
+    } else if (proto == 6u) {
+        put_be16(t, w[11]);
+        put_be16(t + 2, w[11] >> 16);
+        put_be32(t + 4, w[12]);
+        put_be32(t + 8, w[13]);
+        put_be16(t + 12, w[14]);
+        put_be16(t + 14, w[14] >> 16);
+        put_be16(t + 16, l4_ck);
+        put_be16(t + 18, w[15] >> 16);
+    }
+}
+
+// Absolute-phase word sum of LDS slot bytes [s, e) (any alignment): whole dwords,
+// minus the bytes of the first dword below s and of the last dword from e on.
+__device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t s, uint32_t e) {
+    if (e <= s) return 0u;
+    uint32_t acc = 0;
+    for (uint32_t a = s & ~3u; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    acc -= halves(low_bytes(lds32(slot, s & ~3u), s & 3u));
+    if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
+    return acc;
+}
+
+// Store frame bytes [0, r1) (frame-relative, per owning lane) from the tile's LDS
+// slots.  The range lies inside the LDS window (r1 <= kWin - phase).  Each owner lane
+// publishes its frame offset and r1 (W.pref / W.s: free once the stream is done);
+// the lane that stores chunk c = k*64 + lane (piece j = lane & 7 of frame k*8 +
+// lane/8) reads those two words and clips the chunk against the range itself.  A
+// full chunk is one dwordx4, a full dword one dword, the rest byte by byte.
+__device__ __forceinline__ void write_back(uint8_t* frames, WaveScratch& W, int lane,
+                                           uint32_t off, uint32_t r1) {
+    W.pref[lane] = off;
+    W.s[lane] = r1;
+    wave_sync();
+    const int j = lane & (kWinChunks - 1);
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) {
+        const int q = k * (kWave / kWinChunks) + lane / kWinChunks;
+        const uint32_t oq = W.pref[q], rq = W.s[q];
+        const int lo = (int)(oq & 15u) - 16 * j;          // chunk-relative frame start
+        const int hi = lo + (int)rq;                       // chunk-relative range end
+        if (rq == 0 || hi <= 0) continue;
+        const uint32_t base = (oq & ~15u) + 16u * j;       // chunk's absolute address
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&W.win[q * kSlot + 16 * j]);
+        if (lo <= 0 && hi >= 16) {
+            *reinterpret_cast<u32x4*>(frames + base) = u32x4{src[0], src[1], src[2], src[3]};
+            continue;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int dl = lo - 4 * d, dh = hi - 4 * d;     // dword-relative range
+            if (dh <= 0 || dl >= 4) continue;
+            if (dl <= 0 && dh >= 4) {
+                *reinterpret_cast<uint32_t*>(frames + base + 4 * d) = src[d];
+            } else {
+                const uint32_t v = src[d];
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (b >= dl && b < dh) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
+            }
+        }
+    }
+}
+
+// Records of the tile, coalesced: 5 dwordx4 per lane over the tile's contiguous
+// 5 KiB, staged through the window area (stride 21 dwords), then each lane takes its
+// own 20 words.  Must run before the window is committed to LDS.
+__device__ __forceinline__ void load_records_tile(const rpkt_rec_t* recs, uint32_t p0, uint32_t n,
+                                                  WaveScratch& W, int lane, uint32_t (&w)[20]) {
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    const u32x4* in = reinterpret_cast<const u32x4*>(recs + p0);
+    u32x4 v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane;
+        v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+    }
+    uint32_t* st = rec_stage(W);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+        uint32_t* d = st + r * 21 + pc * 4;
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 20; ++k) w[k] = st[lane * 21 + k];
+    wave_sync();
+}
+
+// End (frame-relative) of the range to write back for headers ending at `hdr_end`:
+// extended, with the window's original bytes, to the end of the 128-B cache line
+// (partially written lines cost the memory side a read-modify-write), clipped to the
+// frame and to the LDS window.
+__device__ __forceinline__ uint32_t line_end(Frame fr, uint32_t hdr_end) {
+    const uint32_t ph = fr.off & 15u;
+    const uint32_t line = ((fr.off + hdr_end + 127u) & ~127u) - fr.off;
+    uint32_t e = line < fr.len ? line : fr.len;
+    return e < kWin - ph ? e : kWin - ph;
+}
+
+// rpkt_gpu_build_batch: window -> headers composed in LDS -> checksums (IPv4 over the
+// slot; L4 over the slot plus the payload stream past the window) -> write-back.
+template <bool L4FILL>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
+                  uint32_t stride, uint32_t frame_len, uint32_t n,
+                  const rpkt_rec_t* __restrict__ recs, uint32_t flags, uint8_t* __restrict__ built) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    uint32_t w[20];
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        load_records_tile(recs, p0, n, W, lane, w);             // window loads in flight
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
+    EdgeLines X{false, 0u, 0u, 0u};
+    if constexpr (L4FILL) X = edge_lines_first(rs, fb, W, lane, valid, wend, fend);
+    wave_sync();
+
+    const uint32_t ph = fr.off & 15u, len = fr.len;
+    uint8_t* slot = &W.win[lane * kSlot];
+    const uint32_t nv = (w[0] >> 8) & 0xffu;
+    const uint32_t l3 = 14u + 4u * nv;
+    const uint32_t ihl4 = (w[6] & 0xfu) * 4u;
+    const uint32_t l4 = l3 + ihl4;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;
+    const uint32_t doff4 = ((w[14] >> 12) & 0xfu) * 4u;
+    const uint32_t l4hdr = proto == 17u ? 8u : (proto == 6u ? doff4 : 0u);
+    const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
+    const bool ok = valid && nv <= RPKT_MAX_VLAN && ihl4 >= 20u && !(proto == 6u && doff4 < 20u) &&
+                    len >= l4 + l4hdr && len - l3 <= 65535u &&
+                    !(proto == 17u && len - l4 > 65535u);
+    const bool fill_ip = ok && (flags & RPKT_BUILD_IP_CSUM);
+    const bool fill_l4 = L4FILL && ok && fixed4;
+    if (ok)
+        emit_headers(slot + ph, w, nv, l3, l4, proto, len - l3, len - l4,
+                     fill_ip ? 0u : (w[8] >> 16), fill_l4 ? 0u : (w[15] & 0xffffu));
+    if (fill_ip) {
+        const uint32_t s = be_sum(lds_range_sum(slot, ph + l3, ph + l4), fr.off + l3);
+        put_be16(slot + ph + l3 + 10, ~s & 0xffffu);
+    }
+    if constexpr (L4FILL) {
+        // everything the checksum needs after the stream is packed into the slot's
+        // spare dword (bytes 128..131) and two registers, so the stream keeps its
+        // registers: pseudo header sum, in-window part, and
+        // info = fill | udp << 1 | l4 slot offset << 8
+        uint32_t part = 0, ss = 0, se = 0, pseudo = 0;
+        const uint32_t win_end = kWin - ph;
+        if (fill_l4) {
+            const uint32_t e_in = len < win_end ? len : win_end;
+            part = lds_range_sum(slot, ph + l4, ph + e_in);
+            if (len > e_in) {
+                ss = fr.off + e_in;
+                se = fr.off + len;
+            }
+            const uint32_t src = w[9], dst = w[10];
+            pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto +
+                     (len - l4);
+        }
+        *reinterpret_cast<uint32_t*>(slot + kWin) =
+            (uint32_t)fill_l4 | ((uint32_t)(proto == 17u) << 1) | ((ph + l4) << 8);
+        const uint32_t sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
+        const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
+        if (info & 1u) {
+            const uint32_t at = info >> 8;                      // slot offset of the L4 header
+            const uint32_t sum = fold16(pseudo + be_sum(part + sp, (fr.off & ~15u) + at));
+            uint32_t ck = ~sum & 0xffffu;
+            const bool udp = info & 2u;
+            if (udp && ck == 0u) ck = 0xffffu;                  // RFC 768
+            put_be16(slot + at + (udp ? 6u : 16u), ck);
+        }
+    }
+    wave_sync();
+    // the window holds the original bytes around the headers: round the written range
+    // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
+    const uint32_t r1 = ok ? line_end(fr, l4 + fixed4) : 0u;
+    write_back(frames, W, lane, fr.off, r1);
+    if (built && valid) built[i] = ok ? 1 : 0;
+}
+
+// rpkt_gpu_forward_batch: the loopback_rx loop fused into one pass per frame: header
+// window -> parse (both sums) -> RX verdict -> rewrite in the LDS window -> write-back.
+// Checksums are updated from the verify sums (RFC 1624): swapping addresses and
+// ports leaves every one's-complement sum unchanged, so only the TTL word and the
+// zeroed checksum field move it; both sums are of non-zero data, hence equal to a
+// full recompute bit for bit (the oracle recomputes in full).  The written range is
+// rounded up to whole 16-B chunks inside the frame (the window holds the original
+// payload bytes), so a 64-B frame is rewritten with three dwordx4 stores.
+// V: ablation variant for tools/ablate.py (0 = the product kernel; 1 = no write-back,
+// 2 = parse without the L4 sum, 3 = window + write-back of the whole frame only).
+template <int V>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
+                    uint32_t stride, uint32_t frame_len, uint32_t n, rpkt_fwd_t fwd,
+                    uint8_t* __restrict__ keep) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    WaveScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    wave_sync();
+    if constexpr (V == 3) {
+        write_back(frames, W, lane, fr.off, valid ? line_end(fr, 0u) : 0u);
+        if (valid) keep[i] = 1;
+        return;
+    }
+    LaneRec L;
+    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L);
+    uint8_t* slot = &W.win[lane * kSlot];
+    uint8_t* s = slot + (fr.off & 15u);
+    {
+        // loopback_rx.rs:99-106 before the L4 sum is known: Ok chain, untagged IPv4
+        // (w0 = status | n_vlan << 8 | ethertype << 16), IP checksum good, UDP.  The
+        // rewrite that does not depend on the L4 sum is done in the window now
+        // (written back only if the frame is kept); what the rest needs waits in the
+        // slot's spare dword: pre | l4 << 8 | udp checksum << 16.
+        const uint32_t w0 = L.w[0], w8 = L.w[8], w9 = L.w[9], w10 = L.w[10], w11 = L.w[11];
+        const uint32_t ip_sum = L.w[18] & 0xffffu, l4 = L.w[16] >> 16;
+        const bool pre = valid && (w0 & 0xffffu) == RPKT_S_OK && (w0 >> 16) == 0x0800u &&
+                         ip_sum == 0xffffu && ((w8 >> 8) & 0xffu) == 17u;
+        if (pre) {                                              // loopback_rx.rs:120-133
+            const uint32_t ttl = w8 & 0xffu;
+            const uint32_t old_w = (ttl << 8) | 17u, new_w = (((ttl - 1u) & 0xffu) << 8) | 17u;
+            const uint32_t ip_ck = ~fold16(ip_sum + (~(w8 >> 16) & 0xffffu) +
+                                           (~old_w & 0xffffu) + new_w) & 0xffffu;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                s[k] = fwd.dmac[k];
+                s[6 + k] = fwd.smac[k];
+            }
+            s[22] = (uint8_t)(ttl - 1u);
+            put_be16(s + 24, ip_ck);
+            put_be32(s + 26, w10);
+            put_be32(s + 30, w9);
+            put_be16(s + l4, w11 >> 16);
+            put_be16(s + l4 + 2, w11);
+        }
+        *reinterpret_cast<uint32_t*>(slot + kWin) =
+            (uint32_t)pre | (l4 << 8) | ((L.w[15] & 0xffffu) << 16);
+    }
+    const uint32_t sp = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
+    const uint32_t l4_sum =
+        L.want_l4 ? fold16(L.pseudo + be_sum(L.l4_part + sp, L.l4_start_abs)) : 0u;
+    const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
+    const uint32_t l4 = (info >> 8) & 0xffu, udp_ck = info >> 16;
+    bool fwd_ok = (info & 1u) && (l4_sum == 0xffffu || udp_ck == 0u);   // :107 L4 good
+    if (fwd.n_forbid) {                                         // :111-118, sorted list
+        // up to 128 addresses are searched in LDS (W.s and W.e, contiguous, free once
+        // the stream is done), a longer list in global memory
+        const bool in_lds = fwd.n_forbid <= 2u * kWave;
+        const uint32_t* list = fwd.forbid_dev;
+        if (in_lds) {
+            uint32_t* t = W.s;
+            if ((uint32_t)lane < fwd.n_forbid) t[lane] = fwd.forbid_dev[lane];
+            if ((uint32_t)lane + kWave < fwd.n_forbid) t[lane + kWave] = fwd.forbid_dev[lane + kWave];
+            wave_sync();
+            list = t;
+        }
+        if (fwd_ok) {
+            const uint32_t src = ((uint32_t)s[30] << 24) | ((uint32_t)s[31] << 16) |
+                                 ((uint32_t)s[32] << 8) | s[33];   // swapped: old source
+            uint32_t lo = 0, hi = fwd.n_forbid;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (list[mid] < src) lo = mid + 1; else hi = mid;
+            }
+            if (lo < fwd.n_forbid && list[lo] == src) fwd_ok = false;
+        }
+        wave_sync();
+    }
+    uint32_t r1 = 0;
+    if (fwd_ok) {
+        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu)) & 0xffffu;
+        if (u_ck == 0u) u_ck = 0xffffu;                         // RFC 768
+        put_be16(s + l4 + 6, u_ck);
+        r1 = line_end(fr, l4 + 8u);
+    }
+    wave_sync();
+    if constexpr (V != 1) write_back(frames, W, lane, fr.off, r1);
+    if (valid) keep[i] = fwd_ok ? 1 : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint32_t flags,
+                         uint8_t* built_dev, void* stream) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_BUILD_IP_CSUM | RPKT_BUILD_L4_CSUM)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)b->frames_dev & 15u) != 0)
+        return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true> : build_kernel<false>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
+                  b->stride, flen, b->n, recs_dev, flags, built_dev);
+}
+
+int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
+                           void* stream) {
+    if (!b || !fwd || !keep_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev || (fwd->n_forbid && !fwd->forbid_dev)) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)b->frames_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(forward_kernel<0>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
+                  b->stride, flen, b->n, *fwd, keep_dev);
+}
+
+// Development hook (not part of include/rpkt_gpu.h): forward_kernel ablation variants.
+int rpkt_gpu_debug_forward_variant(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
+                                   int variant, void* stream) {
+    if (!b || !fwd || !keep_dev || b->n == 0) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+#define RPKT_FV(v)                                                                          \
+    launch(forward_kernel<v>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,          \
+           const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,  \
+           b->stride, flen, b->n, *fwd, keep_dev)
+    switch (variant) {
+        case 0: return RPKT_FV(0);
+        case 1: return RPKT_FV(1);
+        case 2: return RPKT_FV(2);
+        case 3: return RPKT_FV(3);
+        default: return RPKT_E_INVAL;
+    }
+#undef RPKT_FV
+}
+
+}  // extern "C"

@@ -1,0 +1,752 @@
+// rpkt_walks.hip — per-frame walks over a batch: the IPv4/TCP option iterators and the
+// protocol-layer walk driven by the pktfmt-derived table.
+#include "rpkt_common.h"
+#include "rpkt_proto_table.h"
+
+namespace {
+
+// ---- option iterators: TcpOptionsIter / Ipv4OptionsIter over a parsed batch ----
+// One wave per 64 frames.  The records give each frame's option slices; only the
+// 16-B chunks that overlap a slice are loaded (frames without options cost their
+// record read and the 64-B output only).  Lane-per-frame walk over LDS bytes with
+// the per-type parse rules of the generated option views (oracle/rpkt_oracle_opts.c
+// cites them); results staged through LDS and stored as 4 KiB of coalesced rows.
+constexpr int kOptChunks = 8;                  // 128 B from the 16-B phase of the first
+constexpr int kOptSlot = 132;                  // option byte: both slices span at most
+                                               // ihl4 + 40 <= 100 B, + 15 of phase
+struct OptScratch {
+    uint8_t win[kWave * kOptSlot];             // 8448 B (stride 33 dwords: conflict-free),
+};                                             // so four blocks (16 waves) fit a CU
+static_assert(kWave * 21 * 4 <= kWave * kOptSlot, "record stage fits the option window");
+
+// Option bytes in LDS: frame byte x of this lane at base[x + bias] (bias = the window's
+// phase minus the first option byte's frame offset; only x >= that offset is read).
+struct OptWin {
+    const uint8_t* base;                       // the lane's slot (4-aligned)
+    uint32_t bias;
+    __device__ __forceinline__ uint32_t b(uint32_t x) const { return base[x + bias]; }
+    // frame bytes x..x+3, little-endian: two aligned LDS dwords and a byte align
+    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
+        const uint32_t y = x + bias, a = y & ~3u;
+        return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
+    }
+    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
+    __device__ __forceinline__ uint32_t be32(uint32_t x) const { return bswap32(dw(x)); }
+};
+
+// returns option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown;
+// d0 = the option's first four bytes (type, length, ...)
+__device__ __forceinline__ int tcp_opt_len(uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
+    switch (t) {
+        case 0: kind = 0; return 1;
+        case 1: kind = 1; return 1;
+        case 2: kind = 2; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 3: kind = 3; return (n >= 3 && hl == 3) ? 3 : 0;
+        case 4: kind = 4; return (n >= 2 && hl == 2) ? 2 : 0;
+        case 5: kind = 5; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        case 8: kind = 6; return (n >= 10 && hl == 10) ? 10 : 0;
+        case 34: kind = 7; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
+        default: return -1;
+    }
+}
+__device__ __forceinline__ int ip_opt_len(uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
+    switch (t) {
+        case 0: kind = 0; return 1;
+        case 1: kind = 1; return 1;
+        case 68: kind = 2; return (n >= 4 && hl >= 4 && hl <= n) ? (int)hl : 0;
+        case 7: kind = 3; return (n >= 3 && hl >= 3 && hl <= n) ? (int)hl : 0;
+        case 148: kind = 4; return (n >= 4 && hl == 4) ? 4 : 0;
+        case 134: kind = 5; return (n >= 6 && hl >= 6 && hl <= n) ? (int)hl : 0;
+        case 137: kind = 6; return (n >= 7 && hl == 7) ? 7 : 0;
+        case 131: kind = 7; return (n >= 7 && hl == 7) ? 7 : 0;
+        default: return -1;
+    }
+}
+
+// One step of a TLV walk (state of Ipv4OptionsIter / TcpOptionsIter): the two walks of
+// a frame are independent, so the kernel steps both in one loop and their LDS round
+// trips overlap.
+struct OptWalk {
+    uint32_t lo, nb, pos, cnt, kinds, stop;
+    uint64_t trace;
+    bool on;
+};
+
+// A run of one-byte options of one type (EOL = kind 0, NOP = kind 1 in both iterators:
+// each is an option of length 1 and the walk goes on) is consumed up to four at a
+// time from the dword at the cursor: padding runs are most of a walk's steps.
+__device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
+    const uint32_t t0 = d0 & 0xffu;
+    if (t0 > 1u) return false;
+    const uint32_t x = d0 ^ (t0 ? 0x01010101u : 0u);   // zero bytes: the same type
+    uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+    k = k < w.nb - w.pos ? k : w.nb - w.pos;            // >= 1: byte 0 matches
+    w.kinds |= 1u << t0;
+    if (w.cnt < 16) {
+        const uint32_t nib = (t0 ? 0x2222u : 0x1111u) & ((1u << (4 * k)) - 1u);   // k <= 4
+        w.trace |= (uint64_t)nib << (4 * w.cnt);
+    }
+    w.cnt += k;
+    w.pos += k;
+    w.on = w.pos < w.nb;
+    return true;
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
+                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                    uint32_t n, const rpkt_rec_t* __restrict__ recs, rpkt_opts_t* __restrict__ opts) {
+    __shared__ __attribute__((aligned(16))) OptScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    OptScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+
+    // records of the tile (coalesced), keep the four words the walks need
+    uint32_t w0, w8, w14, w16;
+    {
+        const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+        const u32x4* in = reinterpret_cast<const u32x4*>(recs + p0);
+        u32x4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t c = k * kWave + lane;
+            v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+        }
+        uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+            uint32_t* d = st + r * 21 + pc * 4;
+            d[0] = v[k].x;
+            d[1] = v[k].y;
+            d[2] = v[k].z;
+            d[3] = v[k].w;
+        }
+        wave_sync();
+        w0 = st[lane * 21 + 0];
+        w8 = st[lane * 21 + 8];
+        w14 = st[lane * 21 + 14];
+        w16 = st[lane * 21 + 16];
+        wave_sync();
+    }
+    const uint32_t status = w0 & 0xffu;
+    const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
+    const bool tcp = status == RPKT_S_OK && ((w8 >> 8) & 0xffu) == 6u;
+    const uint32_t l3 = w16 & 0xffffu, l4 = w16 >> 16;
+    const uint32_t ip_lo = l3 + 20u, ip_hi = ip_parsed ? l4 : ip_lo;
+    const uint32_t t_lo = l4 + 20u, t_hi = tcp ? l4 + ((w14 >> 12) & 0xfu) * 4u : t_lo;
+    // option bytes needed: [lo, hi) of the frame (both slices); chunks outside it skip
+    const uint32_t need_lo = ip_hi > ip_lo ? ip_lo : t_lo;
+    const uint32_t need_hi = t_hi > t_lo ? t_hi : ip_hi;
+    const bool need = (ip_hi > ip_lo) || (t_hi > t_lo);
+
+    // window chunks that overlap the option bytes -> LDS slots
+    {
+        u32x4 d[kOptChunks];
+        uint32_t addr[kOptChunks];
+        uint32_t fix = 0;
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) {
+            const int c = k * kWave + lane;
+            const int q = c / kOptChunks, j = c % kOptChunks;
+            const uint32_t lo = (uint32_t)__shfl((int)(need ? fr.off + need_lo : 0u), q, kWave);
+            const uint32_t hi = (uint32_t)__shfl((int)(need ? fr.off + need_hi : 0u), q, kWave);
+            const uint32_t a = (lo & ~15u) + 16u * j;
+            addr[k] = a < hi ? a : fb;
+            fix |= (uint32_t)straddles(addr[k], fb) << k;
+        }
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+#pragma unroll
+        for (int k = 0; k < kOptChunks; ++k) {
+            const int c = k * kWave + lane;
+            u32x4 v = d[k];
+            if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kOptChunks) * kOptSlot +
+                                                              (c % kOptChunks) * 16]);
+            dst[0] = v.x;
+            dst[1] = v.y;
+            dst[2] = v.z;
+            dst[3] = v.w;
+        }
+    }
+    wave_sync();
+
+    // the two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
+    // TcpOptionsIter::next, tcp/generated.rs:1400-1484), stepped together
+    const OptWin s{&W.win[lane * kOptSlot], ((fr.off + need_lo) & 15u) - need_lo};
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    OptWalk ip{ip_lo, ip_hi - ip_lo, 0, 0, 0, RPKT_OPT_END, 0, ip_parsed && ip_hi > ip_lo};
+    OptWalk tw{t_lo, t_hi - t_lo, 0, 0, 0, RPKT_OPT_END, 0, tcp && t_hi > t_lo};
+    while (ip.on || tw.on) {
+        if (ip.on) {
+            const uint32_t at = ip.lo + ip.pos;
+            const uint32_t d0 = s.dw(at);
+            int kind = 0;
+            const int used = opt_run(ip, d0) ? -2 : ip_opt_len(d0, ip.nb - ip.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
+                ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                ip.on = false;
+            } else {
+                if (kind == 2) o[9] = (o[9] & 0xff000000u) | (d0 >> 8);
+                if (kind == 3) o[8] = (o[8] & 0xffffu) | ((d0 >> 8) << 16);
+                if (kind == 4) o[8] = (o[8] & 0xffff0000u) | be16_hi(d0);
+                if (kind == 5) o[11] = s.be32(at + 2);
+                if (kind == 6 || kind == 7) {
+                    o[9] = (o[9] & 0x00ffffffu) | ((d0 >> 16) << 24);
+                    o[10] = s.be32(at + 3);
+                }
+                ip.kinds |= 1u << kind;
+                if (ip.cnt < 16) ip.trace |= (uint64_t)(kind + 1) << (4 * ip.cnt);
+                ip.cnt += 1;
+                ip.pos += (uint32_t)used;
+                ip.on = ip.pos < ip.nb;
+            }
+        }
+        if (tw.on) {
+            const uint32_t at = tw.lo + tw.pos;
+            const uint32_t d0 = s.dw(at);
+            int kind = 0;
+            const int used = opt_run(tw, d0) ? -2 : tcp_opt_len(d0, tw.nb - tw.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
+                tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                tw.on = false;
+            } else {
+                if (kind == 2) o[1] = (o[1] & 0xffffu) | (be16_hi(d0) << 16);
+                if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (((d0 >> 16) & 0xffu) << 16);
+                if (kind == 5) {
+                    const uint32_t hl = (d0 >> 8) & 0xffu;
+                    o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
+                    o[4] = hl >= 6u ? s.be32(at + 2) : 0u;
+                    o[5] = hl >= 10u ? s.be32(at + 6) : 0u;
+                }
+                if (kind == 6) {
+                    o[2] = s.be32(at + 2);
+                    o[3] = s.be32(at + 6);
+                }
+                if (kind == 7) o[6] = (o[6] & 0xffff0000u) | ((d0 >> 8) & 0xffu);
+                tw.kinds |= 1u << kind;
+                if (tw.cnt < 16) tw.trace |= (uint64_t)(kind + 1) << (4 * tw.cnt);
+                tw.cnt += 1;
+                tw.pos += (uint32_t)used;
+                tw.on = tw.pos < tw.nb;
+            }
+        }
+    }
+    if (ip_parsed) {
+        // word 6: tcp_fo_len | tcp_end << 16 | ip_end << 24; word 7: ip_count | ip_stop << 8 | ip_kinds << 16
+        o[6] |= ip.pos << 24;
+        o[7] = ip.cnt | (ip.stop << 8) | (ip.kinds << 16);
+    }
+    if (tcp) {
+        // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24; word 1: kinds | mss << 16
+        o[0] = (o[0] & 0xffff0000u) | tw.cnt | (tw.stop << 8);
+        o[1] = (o[1] & 0xffff0000u) | tw.kinds;
+        o[6] = (o[6] & 0xff00ffffu) | (tw.pos << 16);
+    }
+    const uint64_t tcp_trace = tw.trace, ip_trace = ip.trace;
+    o[12] = (uint32_t)tcp_trace;
+    o[13] = (uint32_t)(tcp_trace >> 32);
+    o[14] = (uint32_t)ip_trace;
+    o[15] = (uint32_t)(ip_trace >> 32);
+
+    // stage (stride 17 dwords) and store 64 rows of 64 B coalesced
+    wave_sync();
+    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[c]);
+    }
+}
+
+// ---- protocol layer walk: the pktfmt-derived table interpreted per frame ----
+// kProtos / kGroups (rpkt_proto_table.h, generated by tools/pktfmt_table.py from the
+// reference's pktfmt specs) hold, per protocol, exactly what its generated parse /
+// payload / group_parse are functions of; walk_group interprets them with the
+// pktfmt codegen rules (pktfmt/src/codegen/parse.rs:138-244, payload.rs:23-87).
+// One lane per frame over a 128-B LDS window (deeper bytes, about 1 % of the walks of
+// the capture mix, from global memory).  128 B keeps the block at 37 KB of LDS, so four
+// blocks (16 waves) fit a CU: the walk is a chain of dependent LDS round trips, and
+// occupancy is what hides them.
+constexpr int kLayChunks = 8;                  // 128 B window from the 16-B phase
+constexpr int kLaySlot = 132;                  // 33 dwords: conflict-free lanes
+struct LayScratch {
+    uint8_t win[kWave * kLaySlot];             // 8448 B
+};
+
+struct LayerWin {
+    const uint8_t* base;                       // the lane's slot; frame byte x at ph + x
+    uint32_t ph;                               // frame offset & 15
+    uint32_t avail;                            // frame bytes held in LDS
+    uint32_t off;                              // frame's absolute offset
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ uint32_t at(uint32_t x) const {
+        return x < avail ? (uint32_t)base[ph + x] : gbyte(rs, off + x);
+    }
+    // frame bytes x..x+3 as a little-endian dword: two aligned LDS dwords and a byte
+    // align when all four are in the window, else byte by byte
+    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
+        if (x + 4u <= avail) {
+            const uint32_t y = ph + x, a = y & ~3u;
+            return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
+        }
+        return at(x) | (at(x + 1) << 8) | (at(x + 2) << 16) | (at(x + 3) << 24);
+    }
+    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
+    // big-endian bit field (pktfmt bit order) of `bits` <= 32 at bit offset `ob` of x
+    // (cond and length fields are at most 16 bits wide: 4 bytes always cover them)
+    __device__ __forceinline__ uint32_t field(uint32_t x, uint32_t ob, uint32_t bits) const {
+        const uint32_t v = bswap32(dw(x + (ob >> 3)));
+        return (v << (ob & 7u)) >> (32u - bits);
+    }
+};
+
+// The first 20 bytes of the current header as frame-relative little-endian dwords,
+// read once per layer step: every condition, header_len and payload_len field of the
+// table but one (MSTP's, at byte 36) and every dispatch key of lay_next lies in them,
+// so a step costs one round of LDS reads instead of a dependent read per field.
+struct LayHdr {
+    uint32_t F[5];
+};
+
+__device__ __forceinline__ LayHdr lay_hdr(const LayerWin& Wn, uint32_t s) {
+    LayHdr H;
+    if (s + 20u <= Wn.avail) {
+        const uint32_t y = Wn.ph + s, a = y & ~3u;
+        uint32_t R[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) R[k] = lds32(Wn.base, a + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) H.F[k] = align_bytes(R[k + 1], R[k], y & 3u);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) H.F[k] = Wn.dw(s + 4 * k);
+    }
+    return H;
+}
+// header bytes [x, x + 4), x <= 15
+__device__ __forceinline__ uint32_t hdr_dw(const LayHdr& H, uint32_t x) {
+    const uint32_t k = x >> 2;
+    uint32_t lo = H.F[0], hi = H.F[1];
+    lo = k == 1 ? H.F[1] : lo;
+    hi = k == 1 ? H.F[2] : hi;
+    lo = k == 2 ? H.F[2] : lo;
+    hi = k == 2 ? H.F[3] : hi;
+    lo = k == 3 ? H.F[3] : lo;
+    hi = k == 3 ? H.F[4] : hi;
+    return align_bytes(hi, lo, x & 3u);
+}
+__device__ __forceinline__ uint32_t hdr_be16(const LayHdr& H, uint32_t x) {
+    return be16_lo(hdr_dw(H, x));
+}
+__device__ __forceinline__ uint32_t hdr_at(const LayHdr& H, uint32_t x) {
+    return hdr_dw(H, x) & 0xffu;
+}
+// the big-endian bit field of the table at bit offset ob of header s (Wn.field's rule)
+__device__ __forceinline__ uint32_t hdr_field(const LayerWin& Wn, const LayHdr& H, uint32_t s,
+                                              uint32_t ob, uint32_t bits) {
+    if (__builtin_expect((ob >> 3) > 15u, 0)) return Wn.field(s, ob, bits);
+    return (bswap32(hdr_dw(H, ob >> 3)) << (ob & 7u)) >> (32u - bits);
+}
+
+// The walk's LDS image of the table, repacked from kProtos / kGroups at kernel start
+// so that a protocol's scalars are two 16-B reads and a condition one: per protocol
+// 32 B, five 16-B condition slots, one dword per group.
+struct LayProto {
+    uint32_t a;               // hdr | hl_kind << 16 | pl_kind << 24
+    int32_t hl_fixed;
+    uint32_t hl0, hl1;        // expression: off | bits << 16 | form << 24 ; a | b << 16
+    uint32_t pl0, pl1;
+    uint32_t n_cond, pad;
+};
+struct LayCond {
+    uint32_t f;               // off | bits << 16 | n << 24
+    uint32_t lo01, hi01;      // lo[0] | lo[1] << 16 ; hi[0] | hi[1] << 16
+    uint32_t r2;              // lo[2] | hi[2] << 16
+};
+struct LayTable {
+    LayProto p[RPKT_N_PROTOS];
+    LayCond c[RPKT_N_PROTOS][5];
+    uint32_t g[RPKT_N_GROUPS];    // first | count << 8 | cond_bytes << 16 | lut << 24
+    uint32_t lutf[RPKT_N_LUT];    // lookup groups: the keyed field, off | bits << 16
+    uint8_t lut[RPKT_N_LUT][256]; // field value -> member (0xff: none)
+};
+
+__device__ __forceinline__ void lay_table_fill(LayTable& T) {
+    for (uint32_t t = threadIdx.x; t < RPKT_N_PROTOS * 5; t += blockDim.x) {
+        const uint32_t id = t / 5, k = t % 5;
+        const RpktCond& C = kProtos[id].cond[k];
+        T.c[id][k] = LayCond{C.off | ((uint32_t)C.bits << 16) | ((uint32_t)C.n << 24),
+                             C.lo[0] | ((uint32_t)C.lo[1] << 16), C.hi[0] | ((uint32_t)C.hi[1] << 16),
+                             C.lo[2] | ((uint32_t)C.hi[2] << 16)};
+        if (k == 0) {
+            const RpktProto& P = kProtos[id];
+            T.p[id] = LayProto{P.hdr | ((uint32_t)P.hl_kind << 16) | ((uint32_t)P.pl_kind << 24),
+                               P.hl_fixed,
+                               P.hl.off | ((uint32_t)P.hl.bits << 16) | ((uint32_t)P.hl.form << 24),
+                               P.hl.a | ((uint32_t)P.hl.b << 16),
+                               P.pl.off | ((uint32_t)P.pl.bits << 16) | ((uint32_t)P.pl.form << 24),
+                               P.pl.a | ((uint32_t)P.pl.b << 16), P.n_cond, 0u};
+        }
+    }
+    if (threadIdx.x < RPKT_N_GROUPS) {
+        const RpktGroup G = kGroups[threadIdx.x];
+        T.g[threadIdx.x] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
+                           ((uint32_t)G.lut << 24);
+    }
+    if (threadIdx.x < RPKT_N_LUT) T.lutf[threadIdx.x] = kGroupLutField[threadIdx.x];
+    for (uint32_t t = threadIdx.x; t < RPKT_N_LUT * 64; t += blockDim.x)
+        reinterpret_cast<uint32_t*>(T.lut)[t] = reinterpret_cast<const uint32_t*>(kGroupLut)[t];
+}
+
+// pktfmt UsableAlgExpr (ast/length.rs:244-283) of the field at expression e0/e1
+__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H, uint32_t s,
+                                            uint32_t e0, uint32_t e1) {
+    const uint32_t x = hdr_field(Wn, H, s, e0 & 0xffffu, (e0 >> 16) & 0xffu);
+    const uint32_t a = e1 & 0xffffu, b = e1 >> 16;
+    switch (e0 >> 24) {
+        case 0: return x;
+        case 1: return x + a;
+        case 2: return x * a;
+        case 3: return (x + a) * b;
+        default: return x * a + b;
+    }
+}
+
+// group_parse + parse + payload() of group g at cursor [s, e): returns the member
+// protocol (< 0 on Err) with its header length and the trimmed packet end.  A group
+// whose members have no conditions (cond_bytes 0: every group but Ether, VLAN, ICMPv4,
+// GRE, PPPoE and STP) takes its first member without entering the member loop; a
+// group keyed on one byte (ICMPv4 types, PPPoE codes) looks its member up.
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
+                                          uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
+                                          uint32_t& end) {
+    const uint32_t r = e - s;
+    const uint32_t G = T.g[g];
+    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
+    const uint32_t lut = G >> 24;
+    if (r < cond_bytes) return -1;
+    int m = (int)first;
+    if (lut != 0xffu) {                                      // one keyed field: table lookup
+        const uint32_t f = T.lutf[lut];
+        const uint32_t mm = T.lut[lut][hdr_field(Wn, H, s, f & 0xffffu, f >> 16)];
+        if (mm == 0xffu) return -1;
+        m = (int)mm;
+    } else if (cond_bytes) {
+        m = -1;
+        for (uint32_t k = 0; k < count && m < 0; ++k) {
+            const uint32_t id = first + k;
+            const uint32_t nc = T.p[id].n_cond;
+            bool ok = true;
+            for (uint32_t c = 0; c < nc && ok; ++c) {
+                const LayCond C = T.c[id][c];
+                const uint32_t v = hdr_field(Wn, H, s, C.f & 0xffffu, (C.f >> 16) & 0xffu);
+                const uint32_t n = C.f >> 24;
+                bool in = v >= (C.lo01 & 0xffffu) && v <= (C.hi01 & 0xffffu);
+                if (n > 1) in |= v >= (C.lo01 >> 16) && v <= (C.hi01 >> 16);
+                if (n > 2) in |= v >= (C.r2 & 0xffffu) && v <= (C.r2 >> 16);
+                ok = in;
+            }
+            if (ok) m = (int)id;
+        }
+        if (m < 0) return -1;
+    }
+    const LayProto P = T.p[m];
+    const uint32_t hdr = P.a & 0xffffu, hk = (P.a >> 16) & 0xffu, pk = P.a >> 24;
+    if (r < hdr) return -1;
+    uint32_t h = hdr;
+    if (hk == 1) {
+        h = lay_len(Wn, H, s, P.hl0, P.hl1);
+    } else if (hk == 2 || hk == 3) {                        // gre/mod.rs:68-101
+        const uint32_t ind = hdr_be16(H, 0);
+        h = hk == 2 ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
+                          ((ind & 0x1000u) ? 4u : 0u)
+                    : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
+    } else if (hk == 4) {                                   // gtpv1.pktfmt header_len
+        h = (hdr_at(H, 0) & 7u) ? 12u : 8u;
+    } else if (hk == 5) {                                   // gtpv2.pktfmt header_len
+        h = (hdr_at(H, 0) & 8u) ? 12u : 8u;
+    }
+    if (hk) {
+        if (P.hl_fixed >= 0) {
+            if (h != (uint32_t)P.hl_fixed) return -1;
+        } else if (h < hdr || h > r) {
+            return -1;
+        }
+    }
+    end = e;
+    if (pk == 1) {                                          // payload_len
+        const uint32_t pay = lay_len(Wn, H, s, P.pl0, P.pl1);
+        if ((uint64_t)pay + h > r) return -1;
+        end = s + h + pay;
+    } else if (pk == 2) {                                   // packet_len
+        const uint32_t pkt = lay_len(Wn, H, s, P.pl0, P.pl1);
+        if (pkt < h || pkt > r) return -1;
+        end = s + pkt;
+    }
+    hl = h;
+    return m;
+}
+
+constexpr int kNextEnd = -1, kNextUnknown = -2;
+
+__device__ __forceinline__ int lay_ethertype(uint32_t et) {
+    switch (et) {
+        case 0x0800: return RPKT_G_IPV4;
+        case 0x86dd: return RPKT_G_IPV6;
+        case 0x8100: case 0x88a8: return RPKT_G_VLAN;
+        case 0x0806: return RPKT_G_ARP;
+        case 0x8847: case 0x8848: return RPKT_G_MPLS;
+        case 0x8863: case 0x8864: return RPKT_G_PPPOE;
+        default: return kNextUnknown;
+    }
+}
+__device__ __forceinline__ int lay_ipproto(uint32_t p) {
+    switch (p) {
+        case 0: return RPKT_G_IPV6_HOPBYHOP;
+        case 1: return RPKT_G_ICMPV4;
+        case 4: return RPKT_G_IPV4;
+        case 6: return RPKT_G_TCP;
+        case 17: return RPKT_G_UDP;
+        case 41: return RPKT_G_IPV6;
+        case 43: return RPKT_G_IPV6_ROUTING;
+        case 44: return RPKT_G_IPV6_FRAGMENT;
+        case 47: return RPKT_G_GRE;
+        case 51: return RPKT_G_IPV6_AUTH;
+        case 59: return kNextEnd;
+        case 60: return RPKT_G_IPV6_DESTOPTS;
+        default: return kNextUnknown;
+    }
+}
+
+// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
+// starts at h; the cursor is now [s, e).
+__device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, int p, uint32_t s,
+                                        uint32_t e, uint32_t& key) {
+    switch (p) {
+        case RPKT_P_ETHER_ETHERFRAME: key = hdr_be16(H, 12); return lay_ethertype(key);
+        case RPKT_P_VLAN_VLANFRAME: key = hdr_be16(H, 2); return lay_ethertype(key);
+        case RPKT_P_ETHER_ETHERDOT3FRAME: case RPKT_P_VLAN_VLANDOT3FRAME: return RPKT_G_LLC;
+        case RPKT_P_IPV4_IPV4:
+            if (hdr_be16(H, 6) & 0x1fffu) return kNextEnd;          // non-first fragment
+            key = hdr_at(H, 9);
+            return lay_ipproto(key);
+        case RPKT_P_IPV6_IPV6: key = hdr_at(H, 6); return lay_ipproto(key);
+        case RPKT_P_IPV6_FRAGMENTHEADER:
+            if (hdr_be16(H, 2) >> 3) return kNextEnd;
+            key = hdr_at(H, 0);
+            return lay_ipproto(key);
+        case RPKT_P_IPV6_HOPBYHOPOPTION: case RPKT_P_IPV6_DESTOPTIONS:
+        case RPKT_P_IPV6_ROUTINGHEADER: case RPKT_P_IPV6_AUTHENTICATIONHEADER:
+            key = hdr_at(H, 0);
+            return lay_ipproto(key);
+        case RPKT_P_UDP_UDP: {
+            const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0);
+            const uint32_t port = (dp == 4789u || dp == 2152u || dp == 2123u) ? dp
+                                : ((sp == 4789u || sp == 2152u || sp == 2123u) ? sp : 0u);
+            if (!port) return kNextEnd;
+            key = port;
+            if (port == 4789u) return RPKT_G_VXLAN;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 5;                                    // GTP version
+            return key == 1u ? RPKT_G_GTPV1 : (key == 2u ? RPKT_G_GTPV2 : kNextUnknown);
+        }
+        case RPKT_P_GRE_GRE:
+            key = hdr_be16(H, 2);
+            return key == 0x6558u ? RPKT_G_ETHER : lay_ethertype(key);
+        case RPKT_P_VXLAN_VXLAN: return RPKT_G_ETHER;
+        case RPKT_P_GTPV1_GTPV1:
+            if ((hdr_at(H, 0) & 4u) || hdr_at(H, 1) != 255u) return kNextEnd;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 4;
+            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_MPLS_MPLS:
+            if (!(hdr_at(H, 2) & 1u)) return RPKT_G_MPLS;
+            if (e <= s) return kNextEnd;
+            key = Wn.at(s) >> 4;
+            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_PPPOE_PPPOESESSION:
+            key = hdr_be16(H, 6);
+            return key == 0x0021u ? RPKT_G_IPV4 : (key == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
+        case RPKT_P_LLC_LLC:
+            return (hdr_at(H, 0) == 0x42u && hdr_at(H, 1) == 0x42u) ? RPKT_G_STP : kNextEnd;
+        default: return kNextEnd;
+    }
+}
+
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
+                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                   uint32_t n, rpkt_layers_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) LayScratch scratch[kWavesPerBlock];
+    // the protocol table in LDS: lanes walk different protocols, so table reads are
+    // per-lane (divergent) loads; from LDS they cost tens of cycles instead of a
+    // global-memory round trip per dependent lookup
+    __shared__ __attribute__((aligned(16))) LayTable T;
+    lay_table_fill(T);
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    LayScratch& W = scratch[wid];
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    const Frame fr = spans.get(i);
+    {
+        u32x4 d[kLayChunks];
+        uint32_t addr[kLayChunks];
+        uint32_t fix = 0;
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) {
+            const int c = k * kWave + lane;
+            const int q = c / kLayChunks, j = c % kLayChunks;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t ql = (uint32_t)__shfl((int)fr.len, q, kWave);
+            const uint32_t a = (qo & ~15u) + 16u * j;
+            addr[k] = (a < qo + ql) ? a : fb;
+            fix |= (uint32_t)straddles(addr[k], fb) << k;
+        }
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+#pragma unroll
+        for (int k = 0; k < kLayChunks; ++k) {
+            const int c = k * kWave + lane;
+            u32x4 v = d[k];
+            if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kLayChunks) * kLaySlot +
+                                                              (c % kLayChunks) * 16]);
+            dst[0] = v.x;
+            dst[1] = v.y;
+            dst[2] = v.z;
+            dst[3] = v.w;
+        }
+    }
+    wave_sync();
+
+    const uint32_t ph = fr.off & 15u;
+    const LayerWin Wn{&W.win[lane * kLaySlot], ph, (uint32_t)(kLayChunks * 16) - ph, fr.off, rs};
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    uint32_t s = 0, e = valid ? fr.len : 0u, nl = 0, stop = 0, err_g = 0, key = 0, key_p = 0;
+    int g = RPKT_G_ETHER;
+    for (;;) {
+        if (nl == RPKT_MAX_LAYERS) {
+            stop = RPKT_L_MAX;
+            break;
+        }
+        uint32_t hl = 0, end = 0;
+        const LayHdr H = lay_hdr(Wn, s);
+        const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end);
+        if (p < 0) {
+            stop = RPKT_L_ERR;
+            err_g = (uint32_t)g;
+            break;
+        }
+        // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl (predicated: nl differs
+        // per lane, and a runtime register index would be a branch per register)
+        {
+            const uint32_t pw = (uint32_t)p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (nl >> 2) == k ? pw : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (nl >> 1) == k ? sw : 0u;
+        }
+        nl += 1;
+        e = end;
+        s += hl;
+        uint32_t k2 = 0;
+        const int nx = lay_next(Wn, H, p, s, e, k2);
+        if (nx == kNextEnd) {
+            stop = RPKT_L_END;
+            break;
+        }
+        if (nx == kNextUnknown) {
+            stop = RPKT_L_UNKNOWN;
+            key = k2;
+            key_p = (uint32_t)p;
+            break;
+        }
+        g = nx;
+    }
+    o[0] = nl | (stop << 8) | (err_g << 16) | (key_p << 24);
+    o[1] = s & 0xffffu;
+    o[2] = e - s;
+    o[3] = key;
+
+    wave_sync();
+    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* dst = reinterpret_cast<u32x4*>(out + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &dst[c]);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rpkt_gpu_options_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
+                           rpkt_opts_t* opts_dev, void* stream) {
+    if (!b || !recs_dev || !opts_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(options_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  recs_dev, opts_dev);
+}
+
+int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void* stream) {
+    if (!b || !layers_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)layers_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(layers_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  layers_dev);
+}
+
+// Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse
+// kernel and the streaming-copy roofline reference, for tools/ablate.py.
+
+}  // extern "C"
