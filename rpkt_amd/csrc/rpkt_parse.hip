@@ -566,10 +566,12 @@ void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_byte
 }
 
 // ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
-// One workgroup per CU-sized slice of the events; each keeps {pkts, bytes,
-// ip_bad | l4_bad << 16} per bucket in LDS (u32; a slice holds < 65536 events,
-// so no field can overflow), writes it once to its slab, and a second kernel
-// sums the slabs in a fixed order (bitwise reproducible counters).
+// One workgroup per CU-sized slice of the events; each keeps, per bucket in LDS, a
+// u64 {pkts | bytes << 16} (one 64-bit LDS atomic per event; a slice holds at most
+// 32768 events, so pkts never carries into bytes, and 48 bits hold the bytes of any
+// slice) and a u32 {ip_bad | l4_bad << 16}, writes them once to its slab, and a
+// second kernel sums the slabs in a fixed order (bitwise reproducible counters).
+// Slab layout: u64[rows] then u32[rows] (3 * rows dwords).
 constexpr int kFlowThreads = 512;
 constexpr uint32_t kFlowLdsMax = 8192;      // buckets (+1 unparsed row) privatised in LDS
 constexpr uint32_t kFlowMaxPerBlock = 32768;
@@ -588,6 +590,8 @@ void flow_hist_kernel(const uint64_t* __restrict__ ev, uint32_t n, uint32_t per_
                       uint32_t n_buckets, uint32_t* __restrict__ slab) {
     extern __shared__ __attribute__((aligned(16))) uint32_t h[];   // 3 * (n_buckets + 1)
     const uint32_t rows = n_buckets + 1;
+    unsigned long long* pb = reinterpret_cast<unsigned long long*>(h);  // pkts | bytes << 16
+    uint32_t* bad_h = h + 2 * rows;                                     // ip_bad | l4_bad << 16
     for (uint32_t r = threadIdx.x; r < 3 * rows; r += blockDim.x) h[r] = 0;
     __syncthreads();
     const uint32_t lo = blockIdx.x * per_block;
@@ -604,11 +608,10 @@ void flow_hist_kernel(const uint64_t* __restrict__ ev, uint32_t n, uint32_t per_
             if (e[u] == ~0ull) continue;
             uint32_t b = (uint32_t)(e[u] >> 32) & 0xffffu;
             if (b > n_buckets) b = n_buckets;
-            atomicAdd(&h[b], 1u);
-            atomicAdd(&h[rows + b], (uint32_t)e[u]);
+            atomicAdd(&pb[b], 1ull | ((e[u] & 0xffffffffull) << 16));
             const uint32_t bad =
                 (uint32_t)((e[u] >> 48) & 1u) | ((uint32_t)((e[u] >> 49) & 1u) << 16);
-            if (bad) atomicAdd(&h[2 * rows + b], bad);
+            if (bad) atomicAdd(&bad_h[b], bad);
         }
     }
     __syncthreads();
@@ -636,9 +639,10 @@ void flow_reduce_kernel(const uint32_t* __restrict__ slab, uint32_t n_slabs,
     if (b < rows) {
 #pragma unroll 4
         for (uint32_t s = w; s < n_slabs; s += kReduceWaves) {
-            const uint32_t* sl = slab + (size_t)s * 3 * rows;
-            pk += sl[b];
-            by += sl[rows + b];
+            const uint32_t* sl = slab + (size_t)s * 3 * rows;    // 4-B aligned: two dwords
+            const uint64_t v = sl[2 * b] | ((uint64_t)sl[2 * b + 1] << 32);
+            pk += (uint32_t)v & 0xffffu;
+            by += v >> 16;
             const uint32_t bad = sl[2 * rows + b];
             ipb += bad & 0xffffu;
             l4b += bad >> 16;
