@@ -168,6 +168,33 @@ def test_descriptor_past_buffer_is_clamped(torch):
     assert_same(gpu_records(hb), oracle_records(hb))
 
 
+def test_long_tiles_with_ragged_offsets(torch):
+    """1500-B frames packed (tiles over the 64-KB threshold, so the edge lines are
+    summed before the parse) with shifted, empty, negative, overlapping and past-the-end
+    offsets, and IPv4 total lengths short of the frame (Ethernet padding)."""
+    rng = np.random.default_rng(33)
+    base = gen.make_batch(3, 4096, seed=33)
+    offs = (np.arange(base.n + 1, dtype=np.int64) * base.stride)
+    offs[100:] += 7                                   # odd phase from here on
+    offs[200] = offs[199]                             # empty frame
+    offs[300] = offs[299] - 100                       # negative length
+    offs[400] = offs[401] + 3000                      # overlapping the next frames
+    offs[500] = int(offs[-1]) + 10000                 # past the end
+    frames = np.zeros(int(offs[-1]) + 64, dtype=np.uint8)
+    src = base.frames.reshape(base.n, base.stride)
+    for k in range(base.n):                           # lay frame k at its (new) offset
+        o = int(offs[k])
+        if 0 <= o and o + base.stride <= frames.size:
+            frames[o:o + base.stride] = src[k]
+    for k in rng.choice(base.n, 200, replace=False):  # IPv4 tot short of the frame
+        o = int(offs[k])
+        if 0 <= o and o + 18 <= frames.size:
+            frames[o + 16:o + 18] = [0x04, 0x00]
+    offs = np.clip(offs, 0, None).astype(np.uint32)
+    hb = gen.HostBatch(0, base.n, 0, frames, offs, 0, 0)
+    assert_same(gpu_records(hb), oracle_records(hb))
+
+
 def test_jumbo_and_max_length_frames(torch):
     rng = np.random.default_rng(1)
     frames = []
