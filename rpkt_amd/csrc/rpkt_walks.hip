@@ -358,168 +358,39 @@ __device__ __forceinline__ uint32_t hdr_dw(const LayHdr& H, uint32_t x) {
 __device__ __forceinline__ uint32_t hdr_be16(const LayHdr& H, uint32_t x) {
     return be16_lo(hdr_dw(H, x));
 }
-__device__ __forceinline__ uint32_t hdr_at(const LayHdr& H, uint32_t x) {
-    return hdr_dw(H, x) & 0xffu;
-}
-// the big-endian bit field of the table at bit offset ob of header s (Wn.field's rule)
-__device__ __forceinline__ uint32_t hdr_field(const LayerWin& Wn, const LayHdr& H, uint32_t s,
-                                              uint32_t ob, uint32_t bits) {
-    if (__builtin_expect((ob >> 3) > 15u, 0)) return Wn.field(s, ob, bits);
-    return (bswap32(hdr_dw(H, ob >> 3)) << (ob & 7u)) >> (32u - bits);
-}
 
-// The walk's LDS image of the table, repacked from kProtos / kGroups at kernel start
-// so that a protocol's scalars are two 16-B reads and a condition one: per protocol
-// 32 B, five 16-B condition slots, one dword per group.
+// The walk's LDS image of the table, repacked from kProtos / kGroups / kMembers at
+// kernel start.  Lanes walk different protocols, so every step is written as
+// straight-line selects over table values rather than branches on them: a divergent
+// switch costs each wave the union of its cases plus the exec-mask bookkeeping of
+// every case (SALU), which is what bounded the walk.  So a length expression is stored
+// as (x + add) * mul + add2 (covers pktfmt's five forms), a group's members as masked
+// range tests on one dword (kMembers), and the next-layer dispatch as one rule word
+// per protocol (lay_next_rule).
 struct LayProto {
     uint32_t a;               // hdr | hl_kind << 16 | pl_kind << 24
     int32_t hl_fixed;
-    uint32_t hl0, hl1;        // expression: off | bits << 16 | form << 24 ; a | b << 16
-    uint32_t pl0, pl1;
-    uint32_t n_cond, pad;
+    uint32_t hlf, hl_am;      // header_len: field bit off | bits << 16 ; add | mul << 16
+    uint32_t hl_b, plf;       // header_len add2 ; payload field
+    uint32_t pl_am, pl_b;
 };
-struct LayCond {
-    uint32_t f;               // off | bits << 16 | n << 24
-    uint32_t lo01, hi01;      // lo[0] | lo[1] << 16 ; hi[0] | hi[1] << 16
-    uint32_t r2;              // lo[2] | hi[2] << 16
+struct LayMember {
+    uint32_t mask, lo, span, pad;
 };
 struct LayTable {
     LayProto p[RPKT_N_PROTOS];
-    LayCond c[RPKT_N_PROTOS][5];
-    uint32_t g[RPKT_N_GROUPS];    // first | count << 8 | cond_bytes << 16 | lut << 24
-    uint32_t lutf[RPKT_N_LUT];    // lookup groups: the keyed field, off | bits << 16
-    uint8_t lut[RPKT_N_LUT][256]; // field value -> member (0xff: none)
+    LayMember m[RPKT_N_PROTOS + RPKT_MAX_MEMBERS]; // a group's tests read MAX entries
+    uint32_t g[RPKT_N_GROUPS];      // first | count << 8 | cond_bytes << 16 | lut << 24 | key << 28
+    uint32_t nx[RPKT_N_PROTOS];     // next-layer rule (lay_next_rule)
+    int8_t ip[256];                 // IP protocol number -> group / kNextEnd / kNextUnknown
+    uint8_t lut[RPKT_N_LUT][256];   // lookup groups: key byte -> member (0xff: none)
 };
-
-__device__ __forceinline__ void lay_table_fill(LayTable& T) {
-    for (uint32_t t = threadIdx.x; t < RPKT_N_PROTOS * 5; t += blockDim.x) {
-        const uint32_t id = t / 5, k = t % 5;
-        const RpktCond& C = kProtos[id].cond[k];
-        T.c[id][k] = LayCond{C.off | ((uint32_t)C.bits << 16) | ((uint32_t)C.n << 24),
-                             C.lo[0] | ((uint32_t)C.lo[1] << 16), C.hi[0] | ((uint32_t)C.hi[1] << 16),
-                             C.lo[2] | ((uint32_t)C.hi[2] << 16)};
-        if (k == 0) {
-            const RpktProto& P = kProtos[id];
-            T.p[id] = LayProto{P.hdr | ((uint32_t)P.hl_kind << 16) | ((uint32_t)P.pl_kind << 24),
-                               P.hl_fixed,
-                               P.hl.off | ((uint32_t)P.hl.bits << 16) | ((uint32_t)P.hl.form << 24),
-                               P.hl.a | ((uint32_t)P.hl.b << 16),
-                               P.pl.off | ((uint32_t)P.pl.bits << 16) | ((uint32_t)P.pl.form << 24),
-                               P.pl.a | ((uint32_t)P.pl.b << 16), P.n_cond, 0u};
-        }
-    }
-    if (threadIdx.x < RPKT_N_GROUPS) {
-        const RpktGroup G = kGroups[threadIdx.x];
-        T.g[threadIdx.x] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
-                           ((uint32_t)G.lut << 24);
-    }
-    if (threadIdx.x < RPKT_N_LUT) T.lutf[threadIdx.x] = kGroupLutField[threadIdx.x];
-    for (uint32_t t = threadIdx.x; t < RPKT_N_LUT * 64; t += blockDim.x)
-        reinterpret_cast<uint32_t*>(T.lut)[t] = reinterpret_cast<const uint32_t*>(kGroupLut)[t];
-}
-
-// pktfmt UsableAlgExpr (ast/length.rs:244-283) of the field at expression e0/e1
-__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H, uint32_t s,
-                                            uint32_t e0, uint32_t e1) {
-    const uint32_t x = hdr_field(Wn, H, s, e0 & 0xffffu, (e0 >> 16) & 0xffu);
-    const uint32_t a = e1 & 0xffffu, b = e1 >> 16;
-    switch (e0 >> 24) {
-        case 0: return x;
-        case 1: return x + a;
-        case 2: return x * a;
-        case 3: return (x + a) * b;
-        default: return x * a + b;
-    }
-}
-
-// group_parse + parse + payload() of group g at cursor [s, e): returns the member
-// protocol (< 0 on Err) with its header length and the trimmed packet end.  A group
-// whose members have no conditions (cond_bytes 0: every group but Ether, VLAN, ICMPv4,
-// GRE, PPPoE and STP) takes its first member without entering the member loop; a
-// group keyed on one byte (ICMPv4 types, PPPoE codes) looks its member up.
-__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
-                                          uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
-                                          uint32_t& end) {
-    const uint32_t r = e - s;
-    const uint32_t G = T.g[g];
-    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
-    const uint32_t lut = G >> 24;
-    if (r < cond_bytes) return -1;
-    int m = (int)first;
-    if (lut != 0xffu) {                                      // one keyed field: table lookup
-        const uint32_t f = T.lutf[lut];
-        const uint32_t mm = T.lut[lut][hdr_field(Wn, H, s, f & 0xffffu, f >> 16)];
-        if (mm == 0xffu) return -1;
-        m = (int)mm;
-    } else if (cond_bytes) {
-        m = -1;
-        for (uint32_t k = 0; k < count && m < 0; ++k) {
-            const uint32_t id = first + k;
-            const uint32_t nc = T.p[id].n_cond;
-            bool ok = true;
-            for (uint32_t c = 0; c < nc && ok; ++c) {
-                const LayCond C = T.c[id][c];
-                const uint32_t v = hdr_field(Wn, H, s, C.f & 0xffffu, (C.f >> 16) & 0xffu);
-                const uint32_t n = C.f >> 24;
-                bool in = v >= (C.lo01 & 0xffffu) && v <= (C.hi01 & 0xffffu);
-                if (n > 1) in |= v >= (C.lo01 >> 16) && v <= (C.hi01 >> 16);
-                if (n > 2) in |= v >= (C.r2 & 0xffffu) && v <= (C.r2 >> 16);
-                ok = in;
-            }
-            if (ok) m = (int)id;
-        }
-        if (m < 0) return -1;
-    }
-    const LayProto P = T.p[m];
-    const uint32_t hdr = P.a & 0xffffu, hk = (P.a >> 16) & 0xffu, pk = P.a >> 24;
-    if (r < hdr) return -1;
-    uint32_t h = hdr;
-    if (hk == 1) {
-        h = lay_len(Wn, H, s, P.hl0, P.hl1);
-    } else if (hk == 2 || hk == 3) {                        // gre/mod.rs:68-101
-        const uint32_t ind = hdr_be16(H, 0);
-        h = hk == 2 ? 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
-                          ((ind & 0x1000u) ? 4u : 0u)
-                    : 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
-    } else if (hk == 4) {                                   // gtpv1.pktfmt header_len
-        h = (hdr_at(H, 0) & 7u) ? 12u : 8u;
-    } else if (hk == 5) {                                   // gtpv2.pktfmt header_len
-        h = (hdr_at(H, 0) & 8u) ? 12u : 8u;
-    }
-    if (hk) {
-        if (P.hl_fixed >= 0) {
-            if (h != (uint32_t)P.hl_fixed) return -1;
-        } else if (h < hdr || h > r) {
-            return -1;
-        }
-    }
-    end = e;
-    if (pk == 1) {                                          // payload_len
-        const uint32_t pay = lay_len(Wn, H, s, P.pl0, P.pl1);
-        if ((uint64_t)pay + h > r) return -1;
-        end = s + h + pay;
-    } else if (pk == 2) {                                   // packet_len
-        const uint32_t pkt = lay_len(Wn, H, s, P.pl0, P.pl1);
-        if (pkt < h || pkt > r) return -1;
-        end = s + pkt;
-    }
-    hl = h;
-    return m;
-}
+constexpr uint32_t kNoLut = 15;
+static_assert(RPKT_N_LUT < kNoLut, "lookup ids fit 4 bits");
+static_assert(RPKT_N_PROTOS + RPKT_MAX_MEMBERS <= kWave * kWavesPerBlock, "one fill pass");
 
 constexpr int kNextEnd = -1, kNextUnknown = -2;
 
-__device__ __forceinline__ int lay_ethertype(uint32_t et) {
-    switch (et) {
-        case 0x0800: return RPKT_G_IPV4;
-        case 0x86dd: return RPKT_G_IPV6;
-        case 0x8100: case 0x88a8: return RPKT_G_VLAN;
-        case 0x0806: return RPKT_G_ARP;
-        case 0x8847: case 0x8848: return RPKT_G_MPLS;
-        case 0x8863: case 0x8864: return RPKT_G_PPPOE;
-        default: return kNextUnknown;
-    }
-}
 __device__ __forceinline__ int lay_ipproto(uint32_t p) {
     switch (p) {
         case 0: return RPKT_G_IPV6_HOPBYHOP;
@@ -538,59 +409,186 @@ __device__ __forceinline__ int lay_ipproto(uint32_t p) {
     }
 }
 
-// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
-// starts at h; the cursor is now [s, e).
-__device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, int p, uint32_t s,
-                                        uint32_t e, uint32_t& key) {
+// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after each protocol, as a rule:
+// kind | key byte << 4 | fixed group << 8 | flags.  lay_next evaluates it.
+constexpr uint32_t kNxEnd = 0, kNxFixed = 1, kNxEther = 2, kNxIp = 3, kNxUdp = 4,
+                   kNxGtpu = 5, kNxMpls = 6, kNxPpp = 7, kNxLlc = 8;
+constexpr uint32_t kNxTeb = 1u << 16;        // GRE: 0x6558 carries Ethernet
+constexpr uint32_t kNxV4Frag = 1u << 17;     // IPv4: a non-first fragment ends the walk
+constexpr uint32_t kNxV6Frag = 1u << 18;     // IPv6 fragment header: likewise
+__device__ inline uint32_t lay_next_rule(uint32_t p) {
     switch (p) {
-        case RPKT_P_ETHER_ETHERFRAME: key = hdr_be16(H, 12); return lay_ethertype(key);
-        case RPKT_P_VLAN_VLANFRAME: key = hdr_be16(H, 2); return lay_ethertype(key);
-        case RPKT_P_ETHER_ETHERDOT3FRAME: case RPKT_P_VLAN_VLANDOT3FRAME: return RPKT_G_LLC;
-        case RPKT_P_IPV4_IPV4:
-            if (hdr_be16(H, 6) & 0x1fffu) return kNextEnd;          // non-first fragment
-            key = hdr_at(H, 9);
-            return lay_ipproto(key);
-        case RPKT_P_IPV6_IPV6: key = hdr_at(H, 6); return lay_ipproto(key);
-        case RPKT_P_IPV6_FRAGMENTHEADER:
-            if (hdr_be16(H, 2) >> 3) return kNextEnd;
-            key = hdr_at(H, 0);
-            return lay_ipproto(key);
+        case RPKT_P_ETHER_ETHERFRAME: return kNxEther | 12u << 4;
+        case RPKT_P_VLAN_VLANFRAME: return kNxEther | 2u << 4;
+        case RPKT_P_ETHER_ETHERDOT3FRAME: case RPKT_P_VLAN_VLANDOT3FRAME:
+            return kNxFixed | (uint32_t)RPKT_G_LLC << 8;
+        case RPKT_P_IPV4_IPV4: return kNxIp | 9u << 4 | kNxV4Frag;
+        case RPKT_P_IPV6_IPV6: return kNxIp | 6u << 4;
+        case RPKT_P_IPV6_FRAGMENTHEADER: return kNxIp | kNxV6Frag;
         case RPKT_P_IPV6_HOPBYHOPOPTION: case RPKT_P_IPV6_DESTOPTIONS:
-        case RPKT_P_IPV6_ROUTINGHEADER: case RPKT_P_IPV6_AUTHENTICATIONHEADER:
-            key = hdr_at(H, 0);
-            return lay_ipproto(key);
-        case RPKT_P_UDP_UDP: {
-            const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0);
-            const uint32_t port = (dp == 4789u || dp == 2152u || dp == 2123u) ? dp
-                                : ((sp == 4789u || sp == 2152u || sp == 2123u) ? sp : 0u);
-            if (!port) return kNextEnd;
-            key = port;
-            if (port == 4789u) return RPKT_G_VXLAN;
-            if (e <= s) return kNextEnd;
-            key = Wn.at(s) >> 5;                                    // GTP version
-            return key == 1u ? RPKT_G_GTPV1 : (key == 2u ? RPKT_G_GTPV2 : kNextUnknown);
-        }
-        case RPKT_P_GRE_GRE:
-            key = hdr_be16(H, 2);
-            return key == 0x6558u ? RPKT_G_ETHER : lay_ethertype(key);
-        case RPKT_P_VXLAN_VXLAN: return RPKT_G_ETHER;
-        case RPKT_P_GTPV1_GTPV1:
-            if ((hdr_at(H, 0) & 4u) || hdr_at(H, 1) != 255u) return kNextEnd;
-            if (e <= s) return kNextEnd;
-            key = Wn.at(s) >> 4;
-            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
-        case RPKT_P_MPLS_MPLS:
-            if (!(hdr_at(H, 2) & 1u)) return RPKT_G_MPLS;
-            if (e <= s) return kNextEnd;
-            key = Wn.at(s) >> 4;
-            return key == 4u ? RPKT_G_IPV4 : (key == 6u ? RPKT_G_IPV6 : kNextUnknown);
-        case RPKT_P_PPPOE_PPPOESESSION:
-            key = hdr_be16(H, 6);
-            return key == 0x0021u ? RPKT_G_IPV4 : (key == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
-        case RPKT_P_LLC_LLC:
-            return (hdr_at(H, 0) == 0x42u && hdr_at(H, 1) == 0x42u) ? RPKT_G_STP : kNextEnd;
-        default: return kNextEnd;
+        case RPKT_P_IPV6_ROUTINGHEADER: case RPKT_P_IPV6_AUTHENTICATIONHEADER: return kNxIp;
+        case RPKT_P_UDP_UDP: return kNxUdp;
+        case RPKT_P_GRE_GRE: return kNxEther | 2u << 4 | kNxTeb;
+        case RPKT_P_VXLAN_VXLAN: return kNxFixed | (uint32_t)RPKT_G_ETHER << 8;
+        case RPKT_P_GTPV1_GTPV1: return kNxGtpu;
+        case RPKT_P_MPLS_MPLS: return kNxMpls;
+        case RPKT_P_PPPOE_PPPOESESSION: return kNxPpp | 6u << 4;
+        case RPKT_P_LLC_LLC: return kNxLlc;
+        default: return kNxEnd;
     }
+}
+
+// pktfmt UsableAlgExpr (ast/length.rs:244-283): x, x+a, x*a, (x+a)*b, x*a+b as
+// (x + add) * mul + add2, in the same 32-bit arithmetic
+__device__ __forceinline__ void lay_expr(const RpktLenExpr& E, uint32_t& f, uint32_t& am,
+                                         uint32_t& b) {
+    uint32_t add = 0, mul = 1, add2 = 0;
+    switch (E.form) {
+        case 1: add = E.a; break;
+        case 2: mul = E.a; break;
+        case 3: add = E.a; mul = E.b; break;
+        case 4: mul = E.a; add2 = E.b; break;
+        default: break;
+    }
+    f = E.off | ((E.bits ? (uint32_t)E.bits : 32u) << 16);   // 32: unused, no 32-bit shift
+    am = add | (mul << 16);
+    b = add2;
+}
+
+__device__ __forceinline__ void lay_table_fill(LayTable& T) {
+    const uint32_t t = threadIdx.x;
+    if (t < RPKT_N_PROTOS) {
+        const RpktProto& P = kProtos[t];
+        LayProto L;
+        L.a = P.hdr | ((uint32_t)P.hl_kind << 16) | ((uint32_t)P.pl_kind << 24);
+        L.hl_fixed = P.hl_fixed;
+        lay_expr(P.hl, L.hlf, L.hl_am, L.hl_b);
+        lay_expr(P.pl, L.plf, L.pl_am, L.pl_b);
+        T.p[t] = L;
+        T.nx[t] = lay_next_rule(t);
+    }
+    if (t < RPKT_N_PROTOS + RPKT_MAX_MEMBERS) {
+        const RpktMember M = t < RPKT_N_PROTOS ? kMembers[t] : RpktMember{0u, 0u, 0u};
+        T.m[t] = LayMember{M.mask, M.lo, M.span, 0u};
+    }
+    if (t < RPKT_N_GROUPS) {
+        const RpktGroup G = kGroups[t];
+        T.g[t] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
+                 ((G.lut == 0xffu ? kNoLut : (uint32_t)G.lut) << 24) | ((uint32_t)G.key << 28);
+    }
+    if (t < 256) T.ip[t] = (int8_t)lay_ipproto(t);
+    for (uint32_t k = t; k < RPKT_N_LUT * 64; k += blockDim.x)
+        reinterpret_cast<uint32_t*>(T.lut)[k] = reinterpret_cast<const uint32_t*>(kGroupLut)[k];
+}
+
+// the table's length expression at field f of header s
+template <bool kFar>
+__device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H, uint32_t s,
+                                            uint32_t f, uint32_t am, uint32_t b) {
+    const uint32_t ob = f & 0xffffu, bits = (f >> 16) & 0xffu;
+    uint32_t x;
+    if (kFar && __builtin_expect((ob >> 3) > 15u, 0))        // MSTP's, at byte 36
+        x = Wn.field(s, ob, bits);
+    else
+        x = (bswap32(hdr_dw(H, ob >> 3)) << (ob & 7u)) >> (32u - bits);
+    return (x + (am & 0xffffu)) * (am >> 16) + b;
+}
+
+// group_parse + parse + payload() of group g at cursor [s, e): returns the member
+// protocol (< 0 on Err) with its header length and the trimmed packet end.  The
+// members' tests (at most RPKT_MAX_MEMBERS, first match wins, as the generated
+// group_parse tries them in order) run on every lane; a group keyed on one byte
+// (ICMPv4 types, PPPoE codes) looks its member up instead.  Every check folds into
+// one `bad` flag, so the step has no lane-dependent branch.
+__device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
+                                          uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
+                                          uint32_t& end) {
+    const uint32_t r = e - s;
+    const uint32_t G = T.g[g];
+    const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
+    const uint32_t lut = (G >> 24) & 15u;
+    const uint32_t K = bswap32(hdr_dw(H, G >> 28));            // the key dword, big-endian
+    int m = -1;
+#pragma unroll
+    for (uint32_t k = 0; k < RPKT_MAX_MEMBERS; ++k) {
+        const LayMember M = T.m[first + k];
+        const bool hit = k < count && (K & M.mask) - M.lo <= M.span;
+        m = (m < 0 && hit) ? (int)(first + k) : m;
+    }
+    const uint32_t lm = T.lut[lut < RPKT_N_LUT ? lut : 0u][K >> 24];
+    m = lut != kNoLut ? (lm == 0xffu ? -1 : (int)lm) : m;
+    bool bad = r < cond_bytes || m < 0;
+    const LayProto P = T.p[m < 0 ? 0 : m];
+    const uint32_t hdr = P.a & 0xffffu, hk = (P.a >> 16) & 0xffu, pk = P.a >> 24;
+    bad |= r < hdr;
+    const uint32_t ind = hdr_be16(H, 0), b0 = H.F[0] & 0xffu;
+    uint32_t h = lay_len<true>(Wn, H, s, P.hlf, P.hl_am, P.hl_b);
+    // gre/mod.rs:68-101 (GRE, PPTP), gtpv1.pktfmt / gtpv2.pktfmt header_len
+    const uint32_t h_gre = 4u + ((ind & 0xc000u) ? 4u : 0u) + ((ind & 0x2000u) ? 4u : 0u) +
+                           ((ind & 0x1000u) ? 4u : 0u);
+    const uint32_t h_pptp = 8u + ((ind & 0x1000u) ? 4u : 0u) + ((ind & 0x0080u) ? 4u : 0u);
+    h = hk == 2u ? h_gre : h;
+    h = hk == 3u ? h_pptp : h;
+    h = hk == 4u ? ((b0 & 7u) ? 12u : 8u) : h;
+    h = hk == 5u ? ((b0 & 8u) ? 12u : 8u) : h;
+    h = hk == 0u ? hdr : h;
+    bad |= hk != 0u && (P.hl_fixed >= 0 ? h != (uint32_t)P.hl_fixed : (h < hdr || h > r));
+    const uint32_t pl = lay_len<false>(Wn, H, s, P.plf, P.pl_am, P.pl_b);
+    bad |= pk == 1u && (uint64_t)pl + h > r;                 // payload_len
+    bad |= pk == 2u && (pl < h || pl > r);                   // packet_len
+    end = pk == 1u ? s + h + pl : (pk == 2u ? s + pl : e);
+    hl = h;
+    return bad ? -1 : m;
+}
+
+// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
+// starts at h; the cursor is now [s, e).  Every candidate is computed from the header
+// prefix and selected by the protocol's rule kind; key is the unknown next protocol's
+// number when the result is kNextUnknown.
+__device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
+                                        int p, uint32_t s, uint32_t e, uint32_t& key) {
+    const uint32_t R = T.nx[p], kind = R & 15u;
+    const uint32_t k16 = hdr_be16(H, (R >> 4) & 15u), k8 = k16 >> 8;
+    const uint32_t b0 = H.F[0] & 0xffu, b1 = (H.F[0] >> 8) & 0xffu, b2 = (H.F[0] >> 16) & 0xffu;
+    const bool more = e > s;
+    // the payload's first byte: GTP version after UDP, IP version after GTP-U / MPLS
+    uint32_t pb = Wn.base[Wn.ph + (s < Wn.avail ? s : Wn.avail - 1u)];
+    if (__builtin_expect(s >= Wn.avail && more && kind - kNxUdp <= kNxMpls - kNxUdp, 0))
+        pb = gbyte(Wn.rs, Wn.off + s);
+    int eg = kNextUnknown;                                   // EtherType
+    eg = k16 == 0x0800u ? RPKT_G_IPV4 : eg;
+    eg = k16 == 0x86ddu ? RPKT_G_IPV6 : eg;
+    eg = (k16 == 0x8100u || k16 == 0x88a8u) ? RPKT_G_VLAN : eg;
+    eg = k16 == 0x0806u ? RPKT_G_ARP : eg;
+    eg = (k16 == 0x8847u || k16 == 0x8848u) ? RPKT_G_MPLS : eg;
+    eg = (k16 == 0x8863u || k16 == 0x8864u) ? RPKT_G_PPPOE : eg;
+    eg = (k16 == 0x6558u && (R & kNxTeb)) ? RPKT_G_ETHER : eg;
+    const bool frag = ((R & kNxV4Frag) && (hdr_be16(H, 6) & 0x1fffu)) ||
+                      ((R & kNxV6Frag) && (hdr_be16(H, 2) >> 3));
+    const int ig = frag ? kNextEnd : (int)T.ip[k8];          // IP protocol
+    const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0); // UDP: VXLAN / GTP-U / GTP-C
+    const bool dpt = dp == 4789u || dp == 2152u || dp == 2123u;
+    const bool spt = sp == 4789u || sp == 2152u || sp == 2123u;
+    const uint32_t port = dpt ? dp : (spt ? sp : 0u);
+    const uint32_t gv = pb >> 5, iv = pb >> 4;
+    const int gtp = gv == 1u ? RPKT_G_GTPV1 : (gv == 2u ? RPKT_G_GTPV2 : kNextUnknown);
+    const int ipv = iv == 4u ? RPKT_G_IPV4 : (iv == 6u ? RPKT_G_IPV6 : kNextUnknown);
+    const int udp = !port ? kNextEnd : (port == 4789u ? RPKT_G_VXLAN : (more ? gtp : kNextEnd));
+    const int gtpu = ((b0 & 4u) || b1 != 255u || !more) ? kNextEnd : ipv;
+    const int mpls = !(b2 & 1u) ? RPKT_G_MPLS : (more ? ipv : kNextEnd);
+    const int ppp = k16 == 0x0021u ? RPKT_G_IPV4 : (k16 == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
+    const int llc = (b0 == 0x42u && b1 == 0x42u) ? RPKT_G_STP : kNextEnd;
+    int nx = kNextEnd;
+    nx = kind == kNxFixed ? (int)((R >> 8) & 0xffu) : nx;
+    nx = kind == kNxEther ? eg : nx;
+    nx = kind == kNxIp ? ig : nx;
+    nx = kind == kNxUdp ? udp : nx;
+    nx = kind == kNxGtpu ? gtpu : nx;
+    nx = kind == kNxMpls ? mpls : nx;
+    nx = kind == kNxPpp ? ppp : nx;
+    nx = kind == kNxLlc ? llc : nx;
+    key = kind == kNxIp ? k8 : (kind == kNxUdp ? gv : ((kind == kNxGtpu || kind == kNxMpls) ? iv : k16));
+    return nx;
 }
 
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
@@ -652,43 +650,35 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     for (int k = 0; k < 16; ++k) o[k] = 0;
     uint32_t s = 0, e = valid ? fr.len : 0u, nl = 0, stop = 0, err_g = 0, key = 0, key_p = 0;
     int g = RPKT_G_ETHER;
+    // one exit per step: the stop reason is a select chain, so a lane leaving the walk
+    // costs one exec-mask update instead of one per reason
     for (;;) {
-        if (nl == RPKT_MAX_LAYERS) {
-            stop = RPKT_L_MAX;
-            break;
-        }
         uint32_t hl = 0, end = 0;
         const LayHdr H = lay_hdr(Wn, s);
         const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end);
-        if (p < 0) {
-            stop = RPKT_L_ERR;
-            err_g = (uint32_t)g;
-            break;
-        }
+        const bool ok = p >= 0;
         // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl (predicated: nl differs
         // per lane, and a runtime register index would be a branch per register)
         {
             const uint32_t pw = (uint32_t)p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (nl >> 2) == k ? pw : 0u;
+            for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (ok && (nl >> 2) == k) ? pw : 0u;
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (nl >> 1) == k ? sw : 0u;
+            for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (ok && (nl >> 1) == k) ? sw : 0u;
         }
-        nl += 1;
-        e = end;
-        s += hl;
+        nl += ok ? 1u : 0u;
+        e = ok ? end : e;
+        s = ok ? s + hl : s;
         uint32_t k2 = 0;
-        const int nx = lay_next(Wn, H, p, s, e, k2);
-        if (nx == kNextEnd) {
-            stop = RPKT_L_END;
-            break;
-        }
-        if (nx == kNextUnknown) {
-            stop = RPKT_L_UNKNOWN;
-            key = k2;
-            key_p = (uint32_t)p;
-            break;
-        }
+        const int nx = lay_next(Wn, H, T, ok ? p : 0, s, e, k2);
+        stop = !ok                    ? (uint32_t)RPKT_L_ERR
+             : nx == kNextEnd         ? (uint32_t)RPKT_L_END
+             : nx == kNextUnknown     ? (uint32_t)RPKT_L_UNKNOWN
+             : nl == RPKT_MAX_LAYERS  ? (uint32_t)RPKT_L_MAX : 0u;
+        err_g = ok ? 0u : (uint32_t)g;
+        key = ok && nx == kNextUnknown ? k2 : 0u;
+        key_p = ok && nx == kNextUnknown ? (uint32_t)p : 0u;
+        if (stop) break;
         g = nx;
     }
     o[0] = nl | (stop << 8) | (err_g << 16) | (key_p << 24);

@@ -230,7 +230,9 @@ def c_header(t):
          "    uint8_t n_cond;",
          "    RpktCond cond[5];",
          "};",
-         "struct RpktGroup { uint8_t first, count, cond_bytes, lut; };   // lut 0xff: none", ""]
+         "// lut 0xff: none; key: byte offset of the dword the member tests read",
+         "struct RpktGroup { uint8_t first, count, cond_bytes, lut, key; };",
+         "struct RpktMember { uint32_t mask, lo, span; };", ""]
     for g in t["groups"]:
         L.append("#define RPKT_G_%s %d" % (g["name"], t["groups"].index(g)))
     L.append("#define RPKT_N_GROUPS %d" % len(t["groups"]))
@@ -265,7 +267,7 @@ def c_header(t):
     for g in t["groups"]:
         ms = [t["packets"][i] for i in g["members"]]
         f0 = ms[0]["cond"][0] if ms[0]["cond"] else None
-        if (len(ms) > 1 and f0 and f0["bits"] <= 8 and
+        if (len(ms) > 1 and f0 and f0["bits"] == 8 and f0["off"] % 8 == 0 and
                 all(len(m["cond"]) == 1 and m["cond"][0]["off"] == f0["off"] and
                     m["cond"][0]["bits"] == f0["bits"] for m in ms)):
             row = []
@@ -285,10 +287,46 @@ def c_header(t):
     L.append("};")
     L.append("__device__ __constant__ const RpktGroup kGroups[RPKT_N_GROUPS] = {")
     for g in t["groups"]:
-        L.append("    {%d, %d, %d, %d},  // %s" % (g["members"][0], len(g["members"]),
-                                                  g["cond_bytes"], g["lut"], g["name"]))
+        L.append("    {%d, %d, %d, %d, %d},  // %s" % (g["members"][0], len(g["members"]),
+                                                      g["cond_bytes"], g["lut"], g["key"],
+                                                      g["name"]))
+    L.append("};")
+    # Every member's condition as one test on the big-endian dword at its group's key
+    # byte: (key & mask) - lo <= span (unsigned).  A single-range condition on one field
+    # is that field's range shifted into place; several conditions compile only when
+    # each is one exact value (GreForPPTP, the STP BPDUs), which merge into one masked
+    # equality.  A member with no condition has mask 0: it always matches.
+    L.append("#define RPKT_MAX_MEMBERS %d" % max(
+        len(g["members"]) for g in t["groups"] if g["lut"] == 0xFF))
+    L.append("__device__ __constant__ const RpktMember kMembers[RPKT_N_PROTOS] = {")
+    for p in t["packets"]:
+        m = p["member"]
+        L.append("    {0x%08x, 0x%08x, 0x%08x},  // %d %s" % (m[0], m[1], m[2], p["id"], p["name"]))
     L.append("};")
     return "\n".join(L) + "\n"
+
+
+def member_tests(t):
+    """Compile each group's member conditions into masked-dword range tests."""
+    for g in t["groups"]:
+        ms = [t["packets"][i] for i in g["members"]]
+        conds = [c for m in ms for c in m["cond"]]
+        g["key"] = min([c["off"] // 8 for c in conds] or [0])
+        assert g["key"] < 16, g                # the key dword lies in the 20-B header prefix
+        for m in ms:
+            mask = lo = hi = 0
+            for c in m["cond"]:
+                rel = c["off"] - 8 * g["key"]
+                assert rel + c["bits"] <= 32, (m["name"], c)
+                sh = 32 - rel - c["bits"]
+                assert len(c["ranges"]) == 1, (m["name"], c)
+                clo, chi = c["ranges"][0]
+                if len(m["cond"]) > 1:
+                    assert clo == chi, (m["name"], c)
+                mask |= ((1 << c["bits"]) - 1) << sh
+                lo |= clo << sh
+                hi |= chi << sh
+            m["member"] = (mask, lo, hi - lo)
 
 
 def host_header(t):
@@ -316,12 +354,18 @@ def main(ref="/root/reference"):
             assert f["off"] % 8 + f["bits"] <= 32, (p["name"], f)
         for c in p["cond"]:                    # condition fields and ranges are 16-bit
             assert c["bits"] <= 16 and all(0 <= v < 1 << 16 for r in c["ranges"] for v in r)
+        if p["pl"]:                            # payload fields lie in the 20-B prefix
+            assert p["pl"]["off"] // 8 < 16, p["name"]
+    member_tests(t)
     with open(os.path.join(ROOT, "rpkt_amd", "csrc", "rpkt_proto_table.h"), "w") as fh:
         fh.write(c_header(t))
     with open(os.path.join(ROOT, "include", "rpkt_protocols.h"), "w") as fh:
         fh.write(host_header(t))
     for g in t["groups"]:
         g.pop("lut", None)
+        g.pop("key", None)
+    for p in t["packets"]:
+        p.pop("member", None)
     with open(os.path.join(ROOT, "tests", "golden", "proto_table.json"), "w") as fh:
         json.dump(t, fh, indent=1)
     print("%d packets in %d groups" % (len(t["packets"]), len(t["groups"])))
