@@ -279,68 +279,121 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 }
 
 // ---- protocol layer walk: the pktfmt-derived table interpreted per frame ----
-// kProtos / kGroups (rpkt_proto_table.h, generated by tools/pktfmt_table.py from the
-// reference's pktfmt specs) hold, per protocol, exactly what its generated parse /
-// payload / group_parse are functions of; walk_group interprets them with the
+// kProtos / kGroups / kMembers (rpkt_proto_table.h, generated by tools/pktfmt_table.py
+// from the reference's pktfmt specs) hold, per protocol, exactly what its generated
+// parse / payload / group_parse are functions of; walk_group interprets them with the
 // pktfmt codegen rules (pktfmt/src/codegen/parse.rs:138-244, payload.rs:23-87).
-// One lane per frame over a 128-B LDS window (deeper bytes, about 1 % of the walks of
-// the capture mix, from global memory).  128 B keeps the block at 37 KB of LDS, so four
-// blocks (16 waves) fit a CU: the walk is a chain of dependent LDS round trips, and
-// occupancy is what hides them.
-constexpr int kLayChunks = 8;                  // 128 B window from the 16-B phase
+// One lane per frame over a 128-B LDS slot.  128 B keeps the block under 40 KB of LDS,
+// so four blocks (16 waves) fit a CU.  A header that runs past the slot (deep tunnel
+// stacks) refills that lane's slot from the header on, with eight 16-B loads in flight
+// at once.
+//
+// Lanes walk different protocols, so a step is written as straight-line selects over
+// table values rather than branches on them (a divergent switch costs the wave the
+// union of its cases plus exec-mask bookkeeping for each), and the step's LDS reads
+// form a chain of two round trips: the group record (64 B: the group word, its first
+// two member tests and its first member's protocol, whose next-layer rule is folded
+// in), then the next header's first 20 bytes.  Rarer needs (members past the second,
+// the byte-keyed lookup groups, a member other than the first) are read under
+// wave-uniform branches, taken only by waves that have a lane needing them.
+constexpr int kLayChunks = 8;                  // 128 B slot from a 16-B boundary
 constexpr int kLaySlot = 132;                  // 33 dwords: conflict-free lanes
 struct LayScratch {
     uint8_t win[kWave * kLaySlot];             // 8448 B
 };
 
 struct LayerWin {
-    const uint8_t* base;                       // the lane's slot; frame byte x at ph + x
-    uint32_t ph;                               // frame offset & 15
-    uint32_t avail;                            // frame bytes held in LDS
-    uint32_t off;                              // frame's absolute offset
+    uint8_t* base;                             // the lane's slot
+    uint32_t bias;                             // frame byte x at base[x + bias] (mod 2^32)
+    uint32_t avail;                            // frame bytes at or past the cursor and
+                                               // below avail are in the slot
+    uint32_t off, fb;                          // frame's absolute offset; buffer bytes
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ uint32_t at(uint32_t x) const {
-        return x < avail ? (uint32_t)base[ph + x] : gbyte(rs, off + x);
+        return x < avail ? (uint32_t)base[x + bias] : gbyte(rs, off + x);
     }
     // frame bytes x..x+3 as a little-endian dword: two aligned LDS dwords and a byte
-    // align when all four are in the window, else byte by byte
+    // align when all four are in the slot, else byte by byte
     __device__ __forceinline__ uint32_t dw(uint32_t x) const {
         if (x + 4u <= avail) {
-            const uint32_t y = ph + x, a = y & ~3u;
+            const uint32_t y = x + bias, a = y & ~3u;
             return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
         }
         return at(x) | (at(x + 1) << 8) | (at(x + 2) << 16) | (at(x + 3) << 24);
     }
-    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
     // big-endian bit field (pktfmt bit order) of `bits` <= 32 at bit offset `ob` of x
     // (cond and length fields are at most 16 bits wide: 4 bytes always cover them)
     __device__ __forceinline__ uint32_t field(uint32_t x, uint32_t ob, uint32_t bits) const {
         const uint32_t v = bswap32(dw(x + (ob >> 3)));
         return (v << (ob & 7u)) >> (32u - bits);
     }
+    __device__ __forceinline__ void refill(uint32_t s);
 };
 
-// The first 20 bytes of the current header as frame-relative little-endian dwords,
-// read once per layer step: every condition, header_len and payload_len field of the
-// table but one (MSTP's, at byte 36) and every dispatch key of lay_next lies in them,
-// so a step costs one round of LDS reads instead of a dependent read per field.
+// Rare paths of the walk, kept out of line so the loop's hot path stays compact in the
+// instruction cache: a 16-B chunk straddling the buffer end, a field past the header
+// prefix.
+__device__ __attribute__((noinline)) u32x4 lay_edge16(__amdgpu_buffer_rsrc_t rs, uint32_t a,
+                                                      uint32_t fb) {
+    return load16(rs, a, fb);
+}
+// The slot takes the 128 buffer bytes from the 16-B boundary at or below frame byte s
+// (bytes past the buffer read as 0, as gbyte's; at most one chunk straddles its end).
+__device__ __forceinline__ void LayerWin::refill(uint32_t s) {
+    const uint32_t a = (off + s) & ~15u;
+    u32x4 d[kLayChunks];
+    uint32_t fix = 0;
+#pragma unroll
+    for (int k = 0; k < kLayChunks; ++k) {
+        d[k] = load16_fast(rs, a + 16u * k);
+        fix |= (uint32_t)straddles(a + 16u * k, fb) << k;
+    }
+    uint32_t* w = reinterpret_cast<uint32_t*>(base);
+#pragma unroll
+    for (int k = 0; k < kLayChunks; ++k) {
+        w[4 * k] = d[k].x;
+        w[4 * k + 1] = d[k].y;
+        w[4 * k + 2] = d[k].z;
+        w[4 * k + 3] = d[k].w;
+    }
+    if (__builtin_expect(fix != 0, 0)) {
+        const uint32_t k = (uint32_t)__builtin_ctz(fix);
+        const u32x4 v = lay_edge16(rs, a + 16u * k, fb);
+        w[4 * k] = v.x;
+        w[4 * k + 1] = v.y;
+        w[4 * k + 2] = v.z;
+        w[4 * k + 3] = v.w;
+    }
+    bias = off - a;
+    avail = a + 16u * kLayChunks - off;
+}
+__device__ __attribute__((noinline)) uint32_t lay_far_field(uint8_t* base, uint32_t bias,
+                                                            uint32_t avail, uint32_t off,
+                                                            __amdgpu_buffer_rsrc_t rs, uint32_t s,
+                                                            uint32_t ob, uint32_t bits) {
+    const LayerWin Wn{base, bias, avail, off, 0u, rs};     // by value: no address taken
+    return Wn.field(s, ob, bits);
+}
+
+// The first 20 bytes of a header as frame-relative little-endian dwords, read once per
+// layer step: every condition, header_len and payload_len field of the table but one
+// (MSTP's, at byte 36) and every dispatch key of lay_next lies in them.
 struct LayHdr {
     uint32_t F[5];
 };
 
-__device__ __forceinline__ LayHdr lay_hdr(const LayerWin& Wn, uint32_t s) {
+// `fill`: a header past the slot refills it; without, such a header reads as garbage
+// (the caller then never uses it)
+__device__ __forceinline__ LayHdr lay_hdr(LayerWin& Wn, uint32_t s, bool fill) {
+    const bool out = s + 20u > Wn.avail;
+    if (__builtin_expect(out && fill, 0)) Wn.refill(s);
+    const uint32_t y = out && !fill ? 0u : s + Wn.bias, a = y & ~3u;
+    uint32_t R[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) R[k] = lds32(Wn.base, a + 4 * k);
     LayHdr H;
-    if (s + 20u <= Wn.avail) {
-        const uint32_t y = Wn.ph + s, a = y & ~3u;
-        uint32_t R[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) R[k] = lds32(Wn.base, a + 4 * k);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) H.F[k] = align_bytes(R[k + 1], R[k], y & 3u);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) H.F[k] = Wn.dw(s + 4 * k);
-    }
+    for (int k = 0; k < 5; ++k) H.F[k] = align_bytes(R[k + 1], R[k], y & 3u);
     return H;
 }
 // header bytes [x, x + 4), x <= 15
@@ -359,16 +412,12 @@ __device__ __forceinline__ uint32_t hdr_be16(const LayHdr& H, uint32_t x) {
     return be16_lo(hdr_dw(H, x));
 }
 
-// The walk's LDS image of the table, repacked from kProtos / kGroups / kMembers at
-// kernel start.  Lanes walk different protocols, so every step is written as
-// straight-line selects over table values rather than branches on them: a divergent
-// switch costs each wave the union of its cases plus the exec-mask bookkeeping of
-// every case (SALU), which is what bounded the walk.  So a length expression is stored
-// as (x + add) * mul + add2 (covers pktfmt's five forms), a group's members as masked
-// range tests on one dword (kMembers), and the next-layer dispatch as one rule word
-// per protocol (lay_next_rule).
+// The walk's LDS image of the table, built from kProtos / kGroups / kMembers at kernel
+// start.  A length expression is stored as (x + add) * mul + add2 (pktfmt's five forms
+// in the same 32-bit arithmetic), a member's condition as a masked range test on its
+// group's key dword (kMembers), the next-layer dispatch as a 16-bit rule.
 struct LayProto {
-    uint32_t a;               // hdr | hl_kind << 16 | pl_kind << 24
+    uint32_t a;               // hdr | hl_kind << 8 | pl_kind << 12 | next rule << 16
     int32_t hl_fixed;
     uint32_t hlf, hl_am;      // header_len: field bit off | bits << 16 ; add | mul << 16
     uint32_t hl_b, plf;       // header_len add2 ; payload field
@@ -377,45 +426,33 @@ struct LayProto {
 struct LayMember {
     uint32_t mask, lo, span, pad;
 };
+struct __attribute__((aligned(16))) LayGroupRec {
+    LayProto p;               // the first member's protocol
+    uint32_t g;               // first | count << 8 | cond_bytes << 16 | lut << 24 | key << 28
+    uint32_t m0[3];           // member tests of the first two members: mask, lo, span
+    uint32_t m1[3];
+    uint32_t pad;
+};
 struct LayTable {
+    LayGroupRec gr[RPKT_N_GROUPS];
     LayProto p[RPKT_N_PROTOS];
-    LayMember m[RPKT_N_PROTOS + RPKT_MAX_MEMBERS]; // a group's tests read MAX entries
-    uint32_t g[RPKT_N_GROUPS];      // first | count << 8 | cond_bytes << 16 | lut << 24 | key << 28
-    uint32_t nx[RPKT_N_PROTOS];     // next-layer rule (lay_next_rule)
-    int8_t ip[256];                 // IP protocol number -> group / kNextEnd / kNextUnknown
+    LayMember m[RPKT_N_PROTOS + RPKT_MAX_MEMBERS]; // members 2.. read MAX entries
     uint8_t lut[RPKT_N_LUT][256];   // lookup groups: key byte -> member (0xff: none)
 };
 constexpr uint32_t kNoLut = 15;
 static_assert(RPKT_N_LUT < kNoLut, "lookup ids fit 4 bits");
 static_assert(RPKT_N_PROTOS + RPKT_MAX_MEMBERS <= kWave * kWavesPerBlock, "one fill pass");
+static_assert(RPKT_N_GROUPS <= 32, "a rule's fixed group fits 5 bits");
 
 constexpr int kNextEnd = -1, kNextUnknown = -2;
-
-__device__ __forceinline__ int lay_ipproto(uint32_t p) {
-    switch (p) {
-        case 0: return RPKT_G_IPV6_HOPBYHOP;
-        case 1: return RPKT_G_ICMPV4;
-        case 4: return RPKT_G_IPV4;
-        case 6: return RPKT_G_TCP;
-        case 17: return RPKT_G_UDP;
-        case 41: return RPKT_G_IPV6;
-        case 43: return RPKT_G_IPV6_ROUTING;
-        case 44: return RPKT_G_IPV6_FRAGMENT;
-        case 47: return RPKT_G_GRE;
-        case 51: return RPKT_G_IPV6_AUTH;
-        case 59: return kNextEnd;
-        case 60: return RPKT_G_IPV6_DESTOPTS;
-        default: return kNextUnknown;
-    }
-}
 
 // The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after each protocol, as a rule:
 // kind | key byte << 4 | fixed group << 8 | flags.  lay_next evaluates it.
 constexpr uint32_t kNxEnd = 0, kNxFixed = 1, kNxEther = 2, kNxIp = 3, kNxUdp = 4,
                    kNxGtpu = 5, kNxMpls = 6, kNxPpp = 7, kNxLlc = 8;
-constexpr uint32_t kNxTeb = 1u << 16;        // GRE: 0x6558 carries Ethernet
-constexpr uint32_t kNxV4Frag = 1u << 17;     // IPv4: a non-first fragment ends the walk
-constexpr uint32_t kNxV6Frag = 1u << 18;     // IPv6 fragment header: likewise
+constexpr uint32_t kNxTeb = 1u << 13;        // GRE: 0x6558 carries Ethernet
+constexpr uint32_t kNxV4Frag = 1u << 14;     // IPv4: a non-first fragment ends the walk
+constexpr uint32_t kNxV6Frag = 1u << 15;     // IPv6 fragment header: likewise
 __device__ inline uint32_t lay_next_rule(uint32_t p) {
     switch (p) {
         case RPKT_P_ETHER_ETHERFRAME: return kNxEther | 12u << 4;
@@ -439,7 +476,7 @@ __device__ inline uint32_t lay_next_rule(uint32_t p) {
 }
 
 // pktfmt UsableAlgExpr (ast/length.rs:244-283): x, x+a, x*a, (x+a)*b, x*a+b as
-// (x + add) * mul + add2, in the same 32-bit arithmetic
+// (x + add) * mul + add2
 __device__ __forceinline__ void lay_expr(const RpktLenExpr& E, uint32_t& f, uint32_t& am,
                                          uint32_t& b) {
     uint32_t add = 0, mul = 1, add2 = 0;
@@ -455,28 +492,36 @@ __device__ __forceinline__ void lay_expr(const RpktLenExpr& E, uint32_t& f, uint
     b = add2;
 }
 
+__device__ __forceinline__ LayProto lay_proto(uint32_t t) {
+    const RpktProto& P = kProtos[t];
+    LayProto L;
+    L.a = P.hdr | ((uint32_t)P.hl_kind << 8) | ((uint32_t)P.pl_kind << 12) | (lay_next_rule(t) << 16);
+    L.hl_fixed = P.hl_fixed;
+    lay_expr(P.hl, L.hlf, L.hl_am, L.hl_b);
+    lay_expr(P.pl, L.plf, L.pl_am, L.pl_b);
+    return L;
+}
+
 __device__ __forceinline__ void lay_table_fill(LayTable& T) {
     const uint32_t t = threadIdx.x;
-    if (t < RPKT_N_PROTOS) {
-        const RpktProto& P = kProtos[t];
-        LayProto L;
-        L.a = P.hdr | ((uint32_t)P.hl_kind << 16) | ((uint32_t)P.pl_kind << 24);
-        L.hl_fixed = P.hl_fixed;
-        lay_expr(P.hl, L.hlf, L.hl_am, L.hl_b);
-        lay_expr(P.pl, L.plf, L.pl_am, L.pl_b);
-        T.p[t] = L;
-        T.nx[t] = lay_next_rule(t);
-    }
+    if (t < RPKT_N_PROTOS) T.p[t] = lay_proto(t);
     if (t < RPKT_N_PROTOS + RPKT_MAX_MEMBERS) {
         const RpktMember M = t < RPKT_N_PROTOS ? kMembers[t] : RpktMember{0u, 0u, 0u};
         T.m[t] = LayMember{M.mask, M.lo, M.span, 0u};
     }
     if (t < RPKT_N_GROUPS) {
         const RpktGroup G = kGroups[t];
-        T.g[t] = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
-                 ((G.lut == 0xffu ? kNoLut : (uint32_t)G.lut) << 24) | ((uint32_t)G.key << 28);
+        LayGroupRec R;
+        R.p = lay_proto(G.first);
+        R.g = G.first | ((uint32_t)G.count << 8) | ((uint32_t)G.cond_bytes << 16) |
+              ((G.lut == 0xffu ? kNoLut : (uint32_t)G.lut) << 24) | ((uint32_t)G.key << 28);
+        const RpktMember M0 = kMembers[G.first];
+        const RpktMember M1 = G.count > 1 ? kMembers[G.first + 1] : RpktMember{0u, 0u, 0u};
+        R.m0[0] = M0.mask, R.m0[1] = M0.lo, R.m0[2] = M0.span;
+        R.m1[0] = M1.mask, R.m1[1] = M1.lo, R.m1[2] = M1.span;
+        R.pad = 0;
+        T.gr[t] = R;
     }
-    if (t < 256) T.ip[t] = (int8_t)lay_ipproto(t);
     for (uint32_t k = t; k < RPKT_N_LUT * 64; k += blockDim.x)
         reinterpret_cast<uint32_t*>(T.lut)[k] = reinterpret_cast<const uint32_t*>(kGroupLut)[k];
 }
@@ -488,38 +533,60 @@ __device__ __forceinline__ uint32_t lay_len(const LayerWin& Wn, const LayHdr& H,
     const uint32_t ob = f & 0xffffu, bits = (f >> 16) & 0xffu;
     uint32_t x;
     if (kFar && __builtin_expect((ob >> 3) > 15u, 0))        // MSTP's, at byte 36
-        x = Wn.field(s, ob, bits);
+        x = lay_far_field(Wn.base, Wn.bias, Wn.avail, Wn.off, Wn.rs, s, ob, bits);
     else
         x = (bswap32(hdr_dw(H, ob >> 3)) << (ob & 7u)) >> (32u - bits);
     return (x + (am & 0xffffu)) * (am >> 16) + b;
 }
 
+__device__ __forceinline__ bool member_hit(uint32_t K, uint32_t mask, uint32_t lo, uint32_t span) {
+    return (K & mask) - lo <= span;
+}
+
 // group_parse + parse + payload() of group g at cursor [s, e): returns the member
-// protocol (< 0 on Err) with its header length and the trimmed packet end.  The
-// members' tests (at most RPKT_MAX_MEMBERS, first match wins, as the generated
-// group_parse tries them in order) run on every lane; a group keyed on one byte
-// (ICMPv4 types, PPPoE codes) looks its member up instead.  Every check folds into
-// one `bad` flag, so the step has no lane-dependent branch.
+// protocol (< 0 on Err) with its header length, the trimmed packet end and its
+// next-layer rule.  Members are tried in order, the first match wins (the generated
+// group_parse's order); a group keyed on one byte (ICMPv4 types, PPPoE codes) looks
+// its member up.  Every check folds into one `bad` flag.
 __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
                                           uint32_t g, uint32_t s, uint32_t e, uint32_t& hl,
-                                          uint32_t& end) {
+                                          uint32_t& end, uint32_t& rule) {
     const uint32_t r = e - s;
-    const uint32_t G = T.g[g];
+    const LayGroupRec& GR = T.gr[g];
+    LayProto P = GR.p;
+    const uint32_t G = GR.g;
     const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
     const uint32_t lut = (G >> 24) & 15u;
     const uint32_t K = bswap32(hdr_dw(H, G >> 28));            // the key dword, big-endian
-    int m = -1;
+    int m = member_hit(K, GR.m0[0], GR.m0[1], GR.m0[2]) ? (int)first
+          : (count > 1 && member_hit(K, GR.m1[0], GR.m1[1], GR.m1[2])) ? (int)first + 1 : -1;
+    if (__builtin_expect(__ballot(m < 0 && count > 2) != 0, 0)) {      // STP's BPDUs
 #pragma unroll
-    for (uint32_t k = 0; k < RPKT_MAX_MEMBERS; ++k) {
-        const LayMember M = T.m[first + k];
-        const bool hit = k < count && (K & M.mask) - M.lo <= M.span;
-        m = (m < 0 && hit) ? (int)(first + k) : m;
+        for (uint32_t k = 2; k < RPKT_MAX_MEMBERS; ++k) {
+            const LayMember M = T.m[first + k];
+            const bool hit = k < count && member_hit(K, M.mask, M.lo, M.span);
+            m = (m < 0 && hit) ? (int)(first + k) : m;
+        }
     }
-    const uint32_t lm = T.lut[lut < RPKT_N_LUT ? lut : 0u][K >> 24];
-    m = lut != kNoLut ? (lm == 0xffu ? -1 : (int)lm) : m;
+    if (__builtin_expect(__ballot(lut != kNoLut) != 0, 0)) {          // ICMPv4, PPPoE
+        const uint32_t lm = T.lut[lut < RPKT_N_LUT ? lut : 0u][K >> 24];
+        m = lut != kNoLut ? (lm == 0xffu ? -1 : (int)lm) : m;
+    }
+    if (__builtin_expect(__ballot(m > (int)first) != 0, 0)) {         // not the first member
+        // field by field: a select of the whole struct would keep both copies in scratch
+        const bool o = m > (int)first;
+        const LayProto Q = T.p[o ? (uint32_t)m : first];
+        P.a = o ? Q.a : P.a;
+        P.hl_fixed = o ? Q.hl_fixed : P.hl_fixed;
+        P.hlf = o ? Q.hlf : P.hlf;
+        P.hl_am = o ? Q.hl_am : P.hl_am;
+        P.hl_b = o ? Q.hl_b : P.hl_b;
+        P.plf = o ? Q.plf : P.plf;
+        P.pl_am = o ? Q.pl_am : P.pl_am;
+        P.pl_b = o ? Q.pl_b : P.pl_b;
+    }
     bool bad = r < cond_bytes || m < 0;
-    const LayProto P = T.p[m < 0 ? 0 : m];
-    const uint32_t hdr = P.a & 0xffffu, hk = (P.a >> 16) & 0xffu, pk = P.a >> 24;
+    const uint32_t hdr = P.a & 0xffu, hk = (P.a >> 8) & 15u, pk = (P.a >> 12) & 15u;
     bad |= r < hdr;
     const uint32_t ind = hdr_be16(H, 0), b0 = H.F[0] & 0xffu;
     uint32_t h = lay_len<true>(Wn, H, s, P.hlf, P.hl_am, P.hl_b);
@@ -538,23 +605,20 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, c
     bad |= pk == 2u && (pl < h || pl > r);                   // packet_len
     end = pk == 1u ? s + h + pl : (pk == 2u ? s + pl : e);
     hl = h;
+    rule = bad ? kNxEnd : P.a >> 16;
     return bad ? -1 : m;
 }
 
-// The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after protocol p whose header
-// starts at h; the cursor is now [s, e).  Every candidate is computed from the header
-// prefix and selected by the protocol's rule kind; key is the unknown next protocol's
-// number when the result is kNextUnknown.
-__device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, const LayTable& T,
-                                        int p, uint32_t s, uint32_t e, uint32_t& key) {
-    const uint32_t R = T.nx[p], kind = R & 15u;
+// The dispatch after a protocol with rule R whose header H started the step; the cursor
+// is now [s, e) and pb is its first byte.  Every candidate is computed and selected by
+// the rule's kind; key is the unknown next protocol's number when the result is
+// kNextUnknown.
+__device__ __forceinline__ int lay_next(const LayHdr& H, uint32_t pb, uint32_t R, uint32_t s,
+                                        uint32_t e, uint32_t& key) {
+    const uint32_t kind = R & 15u;
     const uint32_t k16 = hdr_be16(H, (R >> 4) & 15u), k8 = k16 >> 8;
     const uint32_t b0 = H.F[0] & 0xffu, b1 = (H.F[0] >> 8) & 0xffu, b2 = (H.F[0] >> 16) & 0xffu;
     const bool more = e > s;
-    // the payload's first byte: GTP version after UDP, IP version after GTP-U / MPLS
-    uint32_t pb = Wn.base[Wn.ph + (s < Wn.avail ? s : Wn.avail - 1u)];
-    if (__builtin_expect(s >= Wn.avail && more && kind - kNxUdp <= kNxMpls - kNxUdp, 0))
-        pb = gbyte(Wn.rs, Wn.off + s);
     int eg = kNextUnknown;                                   // EtherType
     eg = k16 == 0x0800u ? RPKT_G_IPV4 : eg;
     eg = k16 == 0x86ddu ? RPKT_G_IPV6 : eg;
@@ -563,9 +627,22 @@ __device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, con
     eg = (k16 == 0x8847u || k16 == 0x8848u) ? RPKT_G_MPLS : eg;
     eg = (k16 == 0x8863u || k16 == 0x8864u) ? RPKT_G_PPPOE : eg;
     eg = (k16 == 0x6558u && (R & kNxTeb)) ? RPKT_G_ETHER : eg;
+    int ig = kNextUnknown;                                   // IP protocol number
+    ig = k8 == 0u ? RPKT_G_IPV6_HOPBYHOP : ig;
+    ig = k8 == 1u ? RPKT_G_ICMPV4 : ig;
+    ig = k8 == 4u ? RPKT_G_IPV4 : ig;
+    ig = k8 == 6u ? RPKT_G_TCP : ig;
+    ig = k8 == 17u ? RPKT_G_UDP : ig;
+    ig = k8 == 41u ? RPKT_G_IPV6 : ig;
+    ig = k8 == 43u ? RPKT_G_IPV6_ROUTING : ig;
+    ig = k8 == 44u ? RPKT_G_IPV6_FRAGMENT : ig;
+    ig = k8 == 47u ? RPKT_G_GRE : ig;
+    ig = k8 == 51u ? RPKT_G_IPV6_AUTH : ig;
+    ig = k8 == 59u ? kNextEnd : ig;                          // IPv6 no next header
+    ig = k8 == 60u ? RPKT_G_IPV6_DESTOPTS : ig;
     const bool frag = ((R & kNxV4Frag) && (hdr_be16(H, 6) & 0x1fffu)) ||
                       ((R & kNxV6Frag) && (hdr_be16(H, 2) >> 3));
-    const int ig = frag ? kNextEnd : (int)T.ip[k8];          // IP protocol
+    ig = frag ? kNextEnd : ig;
     const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0); // UDP: VXLAN / GTP-U / GTP-C
     const bool dpt = dp == 4789u || dp == 2152u || dp == 2123u;
     const bool spt = sp == 4789u || sp == 2152u || sp == 2123u;
@@ -579,7 +656,7 @@ __device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, con
     const int ppp = k16 == 0x0021u ? RPKT_G_IPV4 : (k16 == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
     const int llc = (b0 == 0x42u && b1 == 0x42u) ? RPKT_G_STP : kNextEnd;
     int nx = kNextEnd;
-    nx = kind == kNxFixed ? (int)((R >> 8) & 0xffu) : nx;
+    nx = kind == kNxFixed ? (int)((R >> 8) & 31u) : nx;
     nx = kind == kNxEther ? eg : nx;
     nx = kind == kNxIp ? ig : nx;
     nx = kind == kNxUdp ? udp : nx;
@@ -591,6 +668,15 @@ __device__ __forceinline__ int lay_next(const LayerWin& Wn, const LayHdr& H, con
     return nx;
 }
 
+// Lane L of a wave walks frames base + L + 64 k, k = 0 .. F-1, one after the other: a
+// walk's depth varies from frame to frame (the capture mix: 2.6 layers on average, a
+// wave's deepest lane 6.8), and a wave runs until its deepest lane ends, so a lane
+// that walks several frames in a row evens the depths out over the wave.  The first
+// frame's window is staged cooperatively (coalesced 16-B loads); a lane's later frames
+// refill its slot.  Records are stored per lane (64 B each).
+constexpr int kLayFrames = 4;
+
+template <int F>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -605,13 +691,13 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     LayScratch& W = scratch[wid];
-    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * (kWave * F);
     if (p0 >= n) return;
-    const uint32_t i = p0 + lane;
-    const bool valid = i < n;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
-    const Frame fr = spans.get(i);
+    Frame fr[F];
+#pragma unroll
+    for (int k = 0; k < F; ++k) fr[k] = spans.get(p0 + lane + kWave * k);
     {
         u32x4 d[kLayChunks];
         uint32_t addr[kLayChunks];
@@ -620,8 +706,8 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         for (int k = 0; k < kLayChunks; ++k) {
             const int c = k * kWave + lane;
             const int q = c / kLayChunks, j = c % kLayChunks;
-            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
-            const uint32_t ql = (uint32_t)__shfl((int)fr.len, q, kWave);
+            const uint32_t qo = (uint32_t)__shfl((int)fr[0].off, q, kWave);
+            const uint32_t ql = (uint32_t)__shfl((int)fr[0].len, q, kWave);
             const uint32_t a = (qo & ~15u) + 16u * j;
             addr[k] = (a < qo + ql) ? a : fb;
             fix |= (uint32_t)straddles(addr[k], fb) << k;
@@ -643,62 +729,89 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
     wave_sync();
 
-    const uint32_t ph = fr.off & 15u;
-    const LayerWin Wn{&W.win[lane * kLaySlot], ph, (uint32_t)(kLayChunks * 16) - ph, fr.off, rs};
+    LayerWin Wn{&W.win[lane * kLaySlot], fr[0].off & 15u, (uint32_t)(kLayChunks * 16) - (fr[0].off & 15u),
+                fr[0].off, fb, rs};
     uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0;
-    uint32_t s = 0, e = valid ? fr.len : 0u, nl = 0, stop = 0, err_g = 0, key = 0, key_p = 0;
+    uint32_t i = p0 + lane;                                  // the lane's current frame
+    bool active = i < n;
+    uint32_t fk = 0;                                         // its index in fr[]
+    uint32_t s = 0, e = fr[0].len, nl = 0;
     int g = RPKT_G_ETHER;
-    // one exit per step: the stop reason is a select chain, so a lane leaving the walk
-    // costs one exec-mask update instead of one per reason
-    for (;;) {
-        uint32_t hl = 0, end = 0;
-        const LayHdr H = lay_hdr(Wn, s);
-        const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end);
-        const bool ok = p >= 0;
-        // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl (predicated: nl differs
-        // per lane, and a runtime register index would be a branch per register)
-        {
-            const uint32_t pw = (uint32_t)p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
+    LayHdr H = lay_hdr(Wn, 0u, false);                      // in the staged window
+    while (__ballot(active)) {
+        uint32_t stop = 0;
+        if (active) {
+            uint32_t hl = 0, end = 0, rule = 0;
+            const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end, rule);
+            const bool ok = p >= 0;
+            // proto[nl] at byte 16 + nl, off[nl] at byte 32 + 2 nl (predicated: nl
+            // differs per lane, and a runtime register index would be a branch per
+            // register)
+            {
+                const uint32_t pw = (uint32_t)p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (ok && (nl >> 2) == k) ? pw : 0u;
+                for (uint32_t k = 0; k < 4; ++k) o[4 + k] |= (ok && (nl >> 2) == k) ? pw : 0u;
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (ok && (nl >> 1) == k) ? sw : 0u;
+                for (uint32_t k = 0; k < 8; ++k) o[8 + k] |= (ok && (nl >> 1) == k) ? sw : 0u;
+            }
+            nl += ok ? 1u : 0u;
+            e = ok ? end : e;
+            s = ok ? s + hl : s;
+            // the next header (its first byte also keys the GTP / IP version dispatch);
+            // a walk that ends here does not refill the slot for it
+            const LayHdr H2 = lay_hdr(Wn, s, (rule & 15u) != kNxEnd);
+            uint32_t k2 = 0;
+            const int nx = lay_next(H, H2.F[0] & 0xffu, rule, s, e, k2);
+            stop = !ok                    ? (uint32_t)RPKT_L_ERR
+                 : nx == kNextEnd         ? (uint32_t)RPKT_L_END
+                 : nx == kNextUnknown     ? (uint32_t)RPKT_L_UNKNOWN
+                 : nl == RPKT_MAX_LAYERS  ? (uint32_t)RPKT_L_MAX : 0u;
+            const uint32_t err_g = ok ? 0u : (uint32_t)g;
+            const bool unk = ok && nx == kNextUnknown;
+            o[0] = nl | (stop << 8) | (err_g << 16) | ((unk ? (uint32_t)p : 0u) << 24);
+            o[1] = s & 0xffffu;
+            o[2] = e - s;
+            o[3] = unk ? k2 : 0u;
+            g = nx;
+            H = H2;
         }
-        nl += ok ? 1u : 0u;
-        e = ok ? end : e;
-        s = ok ? s + hl : s;
-        uint32_t k2 = 0;
-        const int nx = lay_next(Wn, H, T, ok ? p : 0, s, e, k2);
-        stop = !ok                    ? (uint32_t)RPKT_L_ERR
-             : nx == kNextEnd         ? (uint32_t)RPKT_L_END
-             : nx == kNextUnknown     ? (uint32_t)RPKT_L_UNKNOWN
-             : nl == RPKT_MAX_LAYERS  ? (uint32_t)RPKT_L_MAX : 0u;
-        err_g = ok ? 0u : (uint32_t)g;
-        key = ok && nx == kNextUnknown ? k2 : 0u;
-        key_p = ok && nx == kNextUnknown ? (uint32_t)p : 0u;
-        if (stop) break;
-        g = nx;
+        // lanes whose walk ended store their record and move to their next frame
+        if (__ballot(stop != 0)) {
+            if (stop) {
+                u32x4* dst = reinterpret_cast<u32x4*>(out + i);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    __builtin_nontemporal_store(u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]},
+                                                &dst[k]);
+                fk += 1;
+                i += kWave;
+                active = fk < (uint32_t)F && i < n;
+                Frame f = fr[0];
+#pragma unroll
+                for (int k = 1; k < F; ++k) f = fk == (uint32_t)k ? fr[k] : f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) o[k] = 0;
+                s = 0, e = f.len, nl = 0, g = RPKT_G_ETHER;
+                Wn.off = f.off;
+                if (active) {
+                    Wn.refill(0u);
+                    H = lay_hdr(Wn, 0u, false);
+                }
+            }
+        }
     }
-    o[0] = nl | (stop << 8) | (err_g << 16) | (key_p << 24);
-    o[1] = s & 0xffffu;
-    o[2] = e - s;
-    o[3] = key;
+}
 
-    wave_sync();
-    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
-    wave_sync();
-    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
-    u32x4* dst = reinterpret_cast<u32x4*>(out + p0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
-        const uint32_t* src = st + r * 17 + pc * 4;
-        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &dst[c]);
-    }
+template <int F>
+int launch_layers(const rpkt_batch_t* b, uint32_t flen, rpkt_layers_t* layers_dev, void* stream) {
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t waves = (uint32_t)((b->n + (uint64_t)kWave * F - 1) / ((uint64_t)kWave * F));
+    const uint32_t grid = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    return launch(layers_kernel<F>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  layers_dev);
 }
 
 }  // namespace
@@ -729,11 +842,24 @@ int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
     if (((uintptr_t)layers_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint32_t per_block = kWave * kWavesPerBlock;
-    const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(layers_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
-                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
-                  layers_dev);
+    return launch_layers<kLayFrames>(b, flen, layers_dev, stream);
+}
+
+// Development hook (not part of include/rpkt_gpu.h): the walk with F frames per lane
+// (1, 2, 4, 8), for timing the choice of kLayFrames.
+int rpkt_gpu_debug_layers_variant(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, int frames,
+                                  void* stream) {
+    if (!b || !layers_dev || b->n == 0 || !b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    switch (frames) {
+        case 1: return launch_layers<1>(b, flen, layers_dev, stream);
+        case 2: return launch_layers<2>(b, flen, layers_dev, stream);
+        case 4: return launch_layers<4>(b, flen, layers_dev, stream);
+        case 8: return launch_layers<8>(b, flen, layers_dev, stream);
+        default: return RPKT_E_INVAL;
+    }
 }
 
 // Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse
