@@ -438,13 +438,47 @@ struct LayTable {
     LayProto p[RPKT_N_PROTOS];
     LayMember m[RPKT_N_PROTOS + RPKT_MAX_MEMBERS]; // members 2.. read MAX entries
     uint8_t lut[RPKT_N_LUT][256];   // lookup groups: key byte -> member (0xff: none)
+    uint32_t et[32];                // EtherType -> group: ethertype << 8 | group at et_slot()
+    int8_t ip[256];                 // IP protocol number -> group / kNextEnd / kNextUnknown
 };
+// a perfect hash of the ten EtherTypes of the walk into 32 slots (empty: ~0u)
+__device__ __forceinline__ uint32_t et_slot(uint32_t k16) { return ((k16 * 0x36u) >> 8) & 31u; }
 constexpr uint32_t kNoLut = 15;
 static_assert(RPKT_N_LUT < kNoLut, "lookup ids fit 4 bits");
 static_assert(RPKT_N_PROTOS + RPKT_MAX_MEMBERS <= kWave * kWavesPerBlock, "one fill pass");
 static_assert(RPKT_N_GROUPS <= 32, "a rule's fixed group fits 5 bits");
 
 constexpr int kNextEnd = -1, kNextUnknown = -2;
+
+__device__ inline int lay_ethertype(uint32_t et) {
+    switch (et) {
+        case 0x0800: return RPKT_G_IPV4;
+        case 0x86dd: return RPKT_G_IPV6;
+        case 0x8100: case 0x88a8: return RPKT_G_VLAN;
+        case 0x0806: return RPKT_G_ARP;
+        case 0x8847: case 0x8848: return RPKT_G_MPLS;
+        case 0x8863: case 0x8864: return RPKT_G_PPPOE;
+        case 0x6558: return RPKT_G_ETHER;                    // GRE only (kNxTeb)
+        default: return kNextUnknown;
+    }
+}
+__device__ inline int lay_ipproto(uint32_t p) {
+    switch (p) {
+        case 0: return RPKT_G_IPV6_HOPBYHOP;
+        case 1: return RPKT_G_ICMPV4;
+        case 4: return RPKT_G_IPV4;
+        case 6: return RPKT_G_TCP;
+        case 17: return RPKT_G_UDP;
+        case 41: return RPKT_G_IPV6;
+        case 43: return RPKT_G_IPV6_ROUTING;
+        case 44: return RPKT_G_IPV6_FRAGMENT;
+        case 47: return RPKT_G_GRE;
+        case 51: return RPKT_G_IPV6_AUTH;
+        case 59: return kNextEnd;                            // no next header
+        case 60: return RPKT_G_IPV6_DESTOPTS;
+        default: return kNextUnknown;
+    }
+}
 
 // The dispatch of include/rpkt_gpu.h (rpkt_layers_t) after each protocol, as a rule:
 // kind | key byte << 4 | fixed group << 8 | flags.  lay_next evaluates it.
@@ -524,6 +558,15 @@ __device__ __forceinline__ void lay_table_fill(LayTable& T) {
     }
     for (uint32_t k = t; k < RPKT_N_LUT * 64; k += blockDim.x)
         reinterpret_cast<uint32_t*>(T.lut)[k] = reinterpret_cast<const uint32_t*>(kGroupLut)[k];
+    if (t < 256) T.ip[t] = (int8_t)lay_ipproto(t);
+    if (t < 32) {                   // the EtherType hashing to slot t, if any
+        constexpr uint16_t kEt[10] = {0x0800, 0x86dd, 0x8100, 0x88a8, 0x0806,
+                                      0x8847, 0x8848, 0x8863, 0x8864, 0x6558};
+        uint32_t v = ~0u;
+        for (int k = 0; k < 10; ++k)
+            if (et_slot(kEt[k]) == t) v = ((uint32_t)kEt[k] << 8) | (uint32_t)lay_ethertype(kEt[k]);
+        T.et[t] = v;
+    }
 }
 
 // the table's length expression at field f of header s
@@ -558,8 +601,10 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, c
     const uint32_t first = G & 0xffu, count = (G >> 8) & 0xffu, cond_bytes = (G >> 16) & 0xffu;
     const uint32_t lut = (G >> 24) & 15u;
     const uint32_t K = bswap32(hdr_dw(H, G >> 28));            // the key dword, big-endian
-    int m = member_hit(K, GR.m0[0], GR.m0[1], GR.m0[2]) ? (int)first
-          : (count > 1 && member_hit(K, GR.m1[0], GR.m1[1], GR.m1[2])) ? (int)first + 1 : -1;
+    // (bitwise & and |: no short-circuit, so no branch around the second test)
+    const bool hit0 = member_hit(K, GR.m0[0], GR.m0[1], GR.m0[2]);
+    const bool hit1 = (count > 1) & member_hit(K, GR.m1[0], GR.m1[1], GR.m1[2]);
+    int m = hit0 ? (int)first : (hit1 ? (int)first + 1 : -1);
     if (__builtin_expect(__ballot(m < 0 && count > 2) != 0, 0)) {      // STP's BPDUs
 #pragma unroll
         for (uint32_t k = 2; k < RPKT_MAX_MEMBERS; ++k) {
@@ -585,7 +630,7 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, c
         P.pl_am = o ? Q.pl_am : P.pl_am;
         P.pl_b = o ? Q.pl_b : P.pl_b;
     }
-    bool bad = r < cond_bytes || m < 0;
+    bool bad = (r < cond_bytes) | (m < 0);
     const uint32_t hdr = P.a & 0xffu, hk = (P.a >> 8) & 15u, pk = (P.a >> 12) & 15u;
     bad |= r < hdr;
     const uint32_t ind = hdr_be16(H, 0), b0 = H.F[0] & 0xffu;
@@ -599,10 +644,11 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, c
     h = hk == 4u ? ((b0 & 7u) ? 12u : 8u) : h;
     h = hk == 5u ? ((b0 & 8u) ? 12u : 8u) : h;
     h = hk == 0u ? hdr : h;
-    bad |= hk != 0u && (P.hl_fixed >= 0 ? h != (uint32_t)P.hl_fixed : (h < hdr || h > r));
+    const bool hbad = P.hl_fixed >= 0 ? h != (uint32_t)P.hl_fixed : ((h < hdr) | (h > r));
+    bad |= (hk != 0u) & hbad;
     const uint32_t pl = lay_len<false>(Wn, H, s, P.plf, P.pl_am, P.pl_b);
-    bad |= pk == 1u && (uint64_t)pl + h > r;                 // payload_len
-    bad |= pk == 2u && (pl < h || pl > r);                   // packet_len
+    bad |= (pk == 1u) & ((uint64_t)pl + h > r);              // payload_len
+    bad |= (pk == 2u) & ((pl < h) | (pl > r));               // packet_len
     end = pk == 1u ? s + h + pl : (pk == 2u ? s + pl : e);
     hl = h;
     rule = bad ? kNxEnd : P.a >> 16;
@@ -613,48 +659,31 @@ __device__ __forceinline__ int walk_group(const LayerWin& Wn, const LayHdr& H, c
 // is now [s, e) and pb is its first byte.  Every candidate is computed and selected by
 // the rule's kind; key is the unknown next protocol's number when the result is
 // kNextUnknown.
-__device__ __forceinline__ int lay_next(const LayHdr& H, uint32_t pb, uint32_t R, uint32_t s,
-                                        uint32_t e, uint32_t& key) {
+__device__ __forceinline__ int lay_next(const LayHdr& H, const LayTable& T, uint32_t pb, uint32_t R,
+                                        uint32_t s, uint32_t e, uint32_t& key) {
     const uint32_t kind = R & 15u;
     const uint32_t k16 = hdr_be16(H, (R >> 4) & 15u), k8 = k16 >> 8;
     const uint32_t b0 = H.F[0] & 0xffu, b1 = (H.F[0] >> 8) & 0xffu, b2 = (H.F[0] >> 16) & 0xffu;
     const bool more = e > s;
-    int eg = kNextUnknown;                                   // EtherType
-    eg = k16 == 0x0800u ? RPKT_G_IPV4 : eg;
-    eg = k16 == 0x86ddu ? RPKT_G_IPV6 : eg;
-    eg = (k16 == 0x8100u || k16 == 0x88a8u) ? RPKT_G_VLAN : eg;
-    eg = k16 == 0x0806u ? RPKT_G_ARP : eg;
-    eg = (k16 == 0x8847u || k16 == 0x8848u) ? RPKT_G_MPLS : eg;
-    eg = (k16 == 0x8863u || k16 == 0x8864u) ? RPKT_G_PPPOE : eg;
-    eg = (k16 == 0x6558u && (R & kNxTeb)) ? RPKT_G_ETHER : eg;
-    int ig = kNextUnknown;                                   // IP protocol number
-    ig = k8 == 0u ? RPKT_G_IPV6_HOPBYHOP : ig;
-    ig = k8 == 1u ? RPKT_G_ICMPV4 : ig;
-    ig = k8 == 4u ? RPKT_G_IPV4 : ig;
-    ig = k8 == 6u ? RPKT_G_TCP : ig;
-    ig = k8 == 17u ? RPKT_G_UDP : ig;
-    ig = k8 == 41u ? RPKT_G_IPV6 : ig;
-    ig = k8 == 43u ? RPKT_G_IPV6_ROUTING : ig;
-    ig = k8 == 44u ? RPKT_G_IPV6_FRAGMENT : ig;
-    ig = k8 == 47u ? RPKT_G_GRE : ig;
-    ig = k8 == 51u ? RPKT_G_IPV6_AUTH : ig;
-    ig = k8 == 59u ? kNextEnd : ig;                          // IPv6 no next header
-    ig = k8 == 60u ? RPKT_G_IPV6_DESTOPTS : ig;
-    const bool frag = ((R & kNxV4Frag) && (hdr_be16(H, 6) & 0x1fffu)) ||
-                      ((R & kNxV6Frag) && (hdr_be16(H, 2) >> 3));
-    ig = frag ? kNextEnd : ig;
+    const uint32_t E = T.et[et_slot(k16)];                  // EtherType
+    int eg = (E >> 8) == k16 ? (int)(E & 0xffu) : kNextUnknown;
+    eg = (k16 == 0x6558u && !(R & kNxTeb)) ? kNextUnknown : eg;
+    const uint32_t fv = ((R & kNxV4Frag) ? hdr_be16(H, 6) & 0x1fffu : 0u) |
+                        ((R & kNxV6Frag) ? hdr_be16(H, 2) >> 3 : 0u);
+    const bool frag = fv != 0u;
+    const int ig = frag ? kNextEnd : (int)T.ip[k8];          // IP protocol number
     const uint32_t dp = hdr_be16(H, 2), sp = hdr_be16(H, 0); // UDP: VXLAN / GTP-U / GTP-C
-    const bool dpt = dp == 4789u || dp == 2152u || dp == 2123u;
-    const bool spt = sp == 4789u || sp == 2152u || sp == 2123u;
+    const bool dpt = (dp == 4789u) | (dp == 2152u) | (dp == 2123u);
+    const bool spt = (sp == 4789u) | (sp == 2152u) | (sp == 2123u);
     const uint32_t port = dpt ? dp : (spt ? sp : 0u);
     const uint32_t gv = pb >> 5, iv = pb >> 4;
     const int gtp = gv == 1u ? RPKT_G_GTPV1 : (gv == 2u ? RPKT_G_GTPV2 : kNextUnknown);
     const int ipv = iv == 4u ? RPKT_G_IPV4 : (iv == 6u ? RPKT_G_IPV6 : kNextUnknown);
     const int udp = !port ? kNextEnd : (port == 4789u ? RPKT_G_VXLAN : (more ? gtp : kNextEnd));
-    const int gtpu = ((b0 & 4u) || b1 != 255u || !more) ? kNextEnd : ipv;
+    const int gtpu = (((b0 & 4u) != 0u) | (b1 != 255u) | !more) ? kNextEnd : ipv;
     const int mpls = !(b2 & 1u) ? RPKT_G_MPLS : (more ? ipv : kNextEnd);
     const int ppp = k16 == 0x0021u ? RPKT_G_IPV4 : (k16 == 0x0057u ? RPKT_G_IPV6 : kNextUnknown);
-    const int llc = (b0 == 0x42u && b1 == 0x42u) ? RPKT_G_STP : kNextEnd;
+    const int llc = ((b0 == 0x42u) & (b1 == 0x42u)) ? RPKT_G_STP : kNextEnd;
     int nx = kNextEnd;
     nx = kind == kNxFixed ? (int)((R >> 8) & 31u) : nx;
     nx = kind == kNxEther ? eg : nx;
@@ -763,7 +792,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             // a walk that ends here does not refill the slot for it
             const LayHdr H2 = lay_hdr(Wn, s, (rule & 15u) != kNxEnd);
             uint32_t k2 = 0;
-            const int nx = lay_next(H, H2.F[0] & 0xffu, rule, s, e, k2);
+            const int nx = lay_next(H, T, H2.F[0] & 0xffu, rule, s, e, k2);
             stop = !ok                    ? (uint32_t)RPKT_L_ERR
                  : nx == kNextEnd         ? (uint32_t)RPKT_L_END
                  : nx == kNextUnknown     ? (uint32_t)RPKT_L_UNKNOWN
