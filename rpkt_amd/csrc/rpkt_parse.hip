@@ -8,7 +8,9 @@ namespace {
 // One wavefront per 64-frame tile: window loads -> LDS, lane-per-frame parse,
 // flattened L4 stream, LDS-staged coalesced record stores.  (A persistent variant
 // that prefetched the next tile's window into registers measured 1-3 % slower on
-// every config: the extra live registers cost more occupancy than the overlap gave.)
+// every config: the extra live registers cost more occupancy than the overlap gave.
+// Plain loops of 2 or 4 tiles per wave, no prefetch, measured 4-20 % slower:
+// profiles/r01_ablate_tiles_per_wave.log.)
 // L4: compiled with the L4 checksum stream (RPKT_F_L4_SUM).  V: ablation variant for
 // tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
