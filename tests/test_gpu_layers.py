@@ -76,3 +76,36 @@ def test_layers_deep_stacks(torch):
     assert g["n"][:6].tolist() == [3, 4, 5, 6, 7, 8]
     assert (g["stop"][:6] == LAYER_STOP["END"]).all() and g["off"][5][7] > 600
     assert (g["stop"] == LAYER_STOP["MAX"]).sum() == 2
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257, 1000, 4097])
+def test_layers_ragged_batch_sizes(torch, n):
+    """A lane walks frames base + L + 64 k in turn (kLayFrames per lane): batch sizes
+    around the 64-frame tile and the 256-frame wave; no record past n is written."""
+    hb = gen.make_mix(n, seed=900 + n)
+    db = engine.DeviceBatch.from_host(hb)
+    out = torch.full(((n + 64) * 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    engine.layers_batch(db, out=out)
+    o = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets)
+    got = out.cpu().numpy()
+    assert got[:n * 64].tobytes() == o.tobytes()
+    assert (got[n * 64:] == 0xAB).all()
+
+
+def test_layers_frames_per_lane_variants(torch):
+    """The walk with 1, 2, 4 and 8 frames per lane (development hook behind
+    tools/ablate_layers.py) gives the product kernel's records byte for byte."""
+    import ctypes
+    L = engine.lib()
+    L.rpkt_gpu_debug_layers_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_void_p,
+                                                ctypes.c_int, ctypes.c_void_p]
+    L.rpkt_gpu_debug_layers_variant.restype = ctypes.c_int
+    hb = gen.make_mix(20000, seed=77)
+    db = engine.DeviceBatch.from_host(hb)
+    ref = engine.layers_batch(db).cpu().numpy()
+    d = db.desc()
+    for f in (1, 2, 4, 8):
+        out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
+        assert L.rpkt_gpu_debug_layers_variant(ctypes.byref(d), out.data_ptr(), f, None) == 0
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == ref.tobytes(), f
