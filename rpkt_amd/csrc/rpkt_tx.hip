@@ -85,38 +85,59 @@ __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t 
 // slots.  The range lies inside the LDS window (r1 <= kWin - phase).  Each owner lane
 // publishes its frame offset and r1 (W.pref / W.s: free once the stream is done);
 // the lane that stores chunk c = k*64 + lane (piece j = lane & 7 of frame k*8 +
-// lane/8) reads those two words and clips the chunk against the range itself.  A
-// full chunk is one dwordx4, a full dword one dword, the rest byte by byte.
-__device__ __forceinline__ void write_back(uint8_t* frames, WaveScratch& W, int lane,
-                                           uint32_t off, uint32_t r1) {
+// lane/8) reads those two words and clips the chunk against the range itself.
+// A chunk wholly inside the range is one dwordx4 buffer store, issued by every lane:
+// a lane with nothing to store points it past the buffer's range, where the hardware
+// drops it, so the common case has no branch.  Chunks the range cuts (a frame's
+// first chunk at a nonzero 16-B phase, an end inside a chunk) are collected in a mask
+// and stored dword by dword, byte by byte at the cut, behind one wave-uniform branch:
+// bytes outside the range belong to neighbouring frames, which other lanes may be
+// rewriting.
+constexpr uint32_t kDropOffset = 0xffffffe0u;   // past any buffer's range; + 16 does not wrap
+static_assert(kMaxFrameBytes <= kDropOffset, "a dropped store stays out of range");
+__device__ __forceinline__ void write_back(__amdgpu_buffer_rsrc_t rs, uint8_t* frames,
+                                           WaveScratch& W, int lane, uint32_t off, uint32_t r1) {
     W.pref[lane] = off;
     W.s[lane] = r1;
     wave_sync();
     const int j = lane & (kWinChunks - 1);
+    uint32_t cut = 0;
 #pragma unroll
     for (int k = 0; k < kWinChunks; ++k) {
         const int q = k * (kWave / kWinChunks) + lane / kWinChunks;
         const uint32_t oq = W.pref[q], rq = W.s[q];
         const int lo = (int)(oq & 15u) - 16 * j;          // chunk-relative frame start
         const int hi = lo + (int)rq;                       // chunk-relative range end
-        if (rq == 0 || hi <= 0) continue;
+        const bool any = rq != 0 && hi > 0;
+        const bool full = any && lo <= 0 && hi >= 16;
         const uint32_t base = (oq & ~15u) + 16u * j;       // chunk's absolute address
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&W.win[q * kSlot + 16 * j]);
-        if (lo <= 0 && hi >= 16) {
-            *reinterpret_cast<u32x4*>(frames + base) = u32x4{src[0], src[1], src[2], src[3]};
-            continue;
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{src[0], src[1], src[2], src[3]}, rs,
+                                               (int)(full ? base : kDropOffset), 0, 0);
+        cut |= (uint32_t)(any && !full) << k;
+    }
+    if (__builtin_expect(__ballot(cut != 0) != 0, 0)) {
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const int dl = lo - 4 * d, dh = hi - 4 * d;     // dword-relative range
-            if (dh <= 0 || dl >= 4) continue;
-            if (dl <= 0 && dh >= 4) {
-                *reinterpret_cast<uint32_t*>(frames + base + 4 * d) = src[d];
-            } else {
-                const uint32_t v = src[d];
+        for (int k = 0; k < kWinChunks; ++k) {
+            if (!(cut & (1u << k))) continue;
+            const int q = k * (kWave / kWinChunks) + lane / kWinChunks;
+            const uint32_t oq = W.pref[q], rq = W.s[q];
+            const int lo = (int)(oq & 15u) - 16 * j;
+            const int hi = lo + (int)rq;
+            const uint32_t base = (oq & ~15u) + 16u * j;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(&W.win[q * kSlot + 16 * j]);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (b >= dl && b < dh) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
+            for (int d = 0; d < 4; ++d) {
+                const int dl = lo - 4 * d, dh = hi - 4 * d;     // dword-relative range
+                if (dh <= 0 || dl >= 4) continue;
+                if (dl <= 0 && dh >= 4) {
+                    *reinterpret_cast<uint32_t*>(frames + base + 4 * d) = src[d];
+                } else {
+                    const uint32_t v = src[d];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        if (b >= dl && b < dh) frames[base + 4 * d + b] = (uint8_t)(v >> (8 * b));
+                }
             }
         }
     }
@@ -250,7 +271,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     // the window holds the original bytes around the headers: round the written range
     // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
     const uint32_t r1 = ok ? line_end(fr, l4 + fixed4) : 0u;
-    write_back(frames, W, lane, fr.off, r1);
+    write_back(rs, frames, W, lane, fr.off, r1);
     if (built && valid) built[i] = ok ? 1 : 0;
 }
 
@@ -288,7 +309,7 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     }
     wave_sync();
     if constexpr (V == 3) {
-        write_back(frames, W, lane, fr.off, valid ? line_end(fr, 0u) : 0u);
+        write_back(rs, frames, W, lane, fr.off, valid ? line_end(fr, 0u) : 0u);
         if (valid) keep[i] = 1;
         return;
     }
@@ -364,7 +385,7 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         r1 = line_end(fr, l4 + 8u);
     }
     wave_sync();
-    if constexpr (V != 1) write_back(frames, W, lane, fr.off, r1);
+    if constexpr (V != 1) write_back(rs, frames, W, lane, fr.off, r1);
     if (valid) keep[i] = fwd_ok ? 1 : 0;
 }
 
