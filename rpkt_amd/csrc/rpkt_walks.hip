@@ -34,35 +34,43 @@ struct OptWin {
     __device__ __forceinline__ uint32_t be32(uint32_t x) const { return bswap32(dw(x)); }
 };
 
-// returns option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown;
-// d0 = the option's first four bytes (type, length, ...)
-__device__ __forceinline__ int tcp_opt_len(uint32_t d0, uint32_t n, int& kind) {
-    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
+// The per-type parse rules of the generated option views (TcpOptionsIter over
+// tcp/generated.rs, Ipv4OptionsIter over ipv4/generated.rs; oracle/rpkt_oracle_opts.c
+// cites them), as a table per option type read from LDS in the walk (a per-lane type
+// would make a switch divergent): kind index (2..7; 0: not an option type of this
+// iterator) | fixed << 3 | x << 4, where the option needs n >= x remaining bytes and
+// header_len == x (fixed) or x <= header_len <= n.  Types 0 (EOL) and 1 (NOP), kinds
+// 0 and 1 of both iterators, are length-1 options consumed by opt_run.
+__device__ inline uint32_t opt_rule(bool tcp, uint32_t t) {
+    if (tcp) {
+        switch (t) {
+            case 2: return 2u | 8u | 4u << 4;      // Mss
+            case 3: return 3u | 8u | 3u << 4;      // WindowScale
+            case 4: return 4u | 8u | 2u << 4;      // SackPermitted
+            case 5: return 5u | 2u << 4;           // Sack
+            case 8: return 6u | 8u | 10u << 4;     // Timestamp
+            case 34: return 7u | 2u << 4;          // FastOpen
+            default: return 0u;
+        }
+    }
     switch (t) {
-        case 0: kind = 0; return 1;
-        case 1: kind = 1; return 1;
-        case 2: kind = 2; return (n >= 4 && hl == 4) ? 4 : 0;
-        case 3: kind = 3; return (n >= 3 && hl == 3) ? 3 : 0;
-        case 4: kind = 4; return (n >= 2 && hl == 2) ? 2 : 0;
-        case 5: kind = 5; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
-        case 8: kind = 6; return (n >= 10 && hl == 10) ? 10 : 0;
-        case 34: kind = 7; return (n >= 2 && hl >= 2 && hl <= n) ? (int)hl : 0;
-        default: return -1;
+        case 68: return 2u | 4u << 4;              // Timestamp
+        case 7: return 3u | 3u << 4;               // RecordRoute
+        case 148: return 4u | 8u | 4u << 4;        // RouteAlert
+        case 134: return 5u | 6u << 4;             // CommercialSecurity
+        case 137: return 6u | 8u | 7u << 4;        // StrictSourceRoute
+        case 131: return 7u | 8u | 7u << 4;        // LooseSourceRoute
+        default: return 0u;
     }
 }
-__device__ __forceinline__ int ip_opt_len(uint32_t d0, uint32_t n, int& kind) {
-    const uint32_t t = d0 & 0xffu, hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
-    switch (t) {
-        case 0: kind = 0; return 1;
-        case 1: kind = 1; return 1;
-        case 68: kind = 2; return (n >= 4 && hl >= 4 && hl <= n) ? (int)hl : 0;
-        case 7: kind = 3; return (n >= 3 && hl >= 3 && hl <= n) ? (int)hl : 0;
-        case 148: kind = 4; return (n >= 4 && hl == 4) ? 4 : 0;
-        case 134: kind = 5; return (n >= 6 && hl >= 6 && hl <= n) ? (int)hl : 0;
-        case 137: kind = 6; return (n >= 7 && hl == 7) ? 7 : 0;
-        case 131: kind = 7; return (n >= 7 && hl == 7) ? 7 : 0;
-        default: return -1;
-    }
+// option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown type
+__device__ __forceinline__ int opt_len(uint32_t rule, uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
+    const uint32_t x = rule >> 4;
+    const bool fixed = (rule & 8u) != 0u;
+    const bool ok = (n >= x) & (fixed ? hl == x : (hl >= x) & (hl <= n));
+    kind = (int)(rule & 7u);
+    return (rule & 7u) == 0u ? -1 : (ok ? (int)(fixed ? x : hl) : 0);
 }
 
 // One step of a TLV walk (state of Ipv4OptionsIter / TcpOptionsIter): the two walks of
@@ -99,6 +107,14 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                     uint32_t n, const rpkt_rec_t* __restrict__ recs, rpkt_opts_t* __restrict__ opts) {
     __shared__ __attribute__((aligned(16))) OptScratch scratch[kWavesPerBlock];
+    // the option-type rules of both iterators (a per-lane type: LDS, not a switch)
+    __shared__ uint8_t rules[2][256];
+    static_assert(kWave * kWavesPerBlock >= 256, "one fill pass");
+    if (threadIdx.x < 256) {
+        rules[0][threadIdx.x] = (uint8_t)opt_rule(false, threadIdx.x);
+        rules[1][threadIdx.x] = (uint8_t)opt_rule(true, threadIdx.x);
+    }
+    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     OptScratch& W = scratch[wid];
@@ -193,7 +209,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             const uint32_t at = ip.lo + ip.pos;
             const uint32_t d0 = s.dw(at);
             int kind = 0;
-            const int used = opt_run(ip, d0) ? -2 : ip_opt_len(d0, ip.nb - ip.pos, kind);
+            const int used = opt_run(ip, d0) ? -2 : opt_len(rules[0][d0 & 0xffu], d0, ip.nb - ip.pos, kind);
             if (used == -2) {
             } else if (used <= 0) {
                 ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
@@ -218,7 +234,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             const uint32_t at = tw.lo + tw.pos;
             const uint32_t d0 = s.dw(at);
             int kind = 0;
-            const int used = opt_run(tw, d0) ? -2 : tcp_opt_len(d0, tw.nb - tw.pos, kind);
+            const int used = opt_run(tw, d0) ? -2 : opt_len(rules[1][d0 & 0xffu], d0, tw.nb - tw.pos, kind);
             if (used == -2) {
             } else if (used <= 0) {
                 tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
