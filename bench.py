@@ -156,6 +156,20 @@ def pmc_traffic(cfg):
     return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
 
 
+def pmc_traffic_tx(leg):
+    """Per-launch HBM traffic of a TX / walk leg (profiles/traffic_tx.json, from a
+    rocprofv3 PMC profile of those legs on this exact engine build); else None."""
+    path = os.path.join(ROOT, "profiles", "traffic_tx.json")
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("engine_build") != engine.lib().rpkt_gpu_build_info().decode() or leg not in t["legs"]:
+        return None, None
+    return int(t["legs"][leg]["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
 def head_sample(hb, max_bytes=256 << 20):
     """The first frames of a host batch, at most ~max_bytes of frame data."""
     lens = hb.lens()
@@ -403,11 +417,13 @@ def run_tx(cfg, mode, args, rank, world):
         kept = outs[0].cpu().numpy().astype(bool)
         alg = int(lens.sum()) + hbs[0].n + int(kept.sum()) * 42
     achieved = alg / (kern_ms / 1e3) / 1e9
+    traffic, tsrc = pmc_traffic_tx("%s%d" % (mode, cfg))      # the bench leg's name
     return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
             "ms_per_step": wall / args.steps * 1e3, "frames_per_rank": hbs[0].n,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "alg_bytes_per_launch": alg},
+                         "alg_bytes_per_launch": alg, "traffic": traffic,
+                         "traffic_source": tsrc},
             "what": ("build: Udp|Tcp/Ipv4/Ether prepend_header + setters, IPv4 + L4 checksum "
                      "fill" if mode == "build" else
                      "options: Ipv4OptionsIter + TcpOptionsIter walks of a parsed batch"

@@ -5,6 +5,9 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half of 
 wide coalesced streaming read (MI355X_MICROARCH.md §HBM), so the read side is
 doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
 Usage: python tools/traffic.py <prof_dir> <config> <out_json>
+       python tools/traffic.py <prof_dir> tx <out_json>
+  (tx: a profile of `bench.py --tx build2,forward2,opts5,layers9`, one kernel per leg:
+   the TX and walk kernels' traffic per launch, keyed by bench leg)
 """
 import csv
 import json
@@ -54,5 +57,39 @@ def main(prof, cfg, out):
     print(json.dumps({k: v for k, v in res.items() if k != "kernel_stats"}))
 
 
+TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "options_kernel",
+           "layers9": "layers_kernel"}
+
+
+def main_tx(prof, out):
+    def pmc(name, kname):
+        v = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, name + "_counter_collection.csv"))
+             if r["Kernel_Name"].startswith(kname)][5:]
+        return sum(v) / len(v) if v else None
+
+    build = None
+    with open(os.path.join(prof, "trace_bench.log")) as fh:
+        for line in fh:
+            if line.startswith("{"):
+                build = json.loads(line).get("engine_build")
+    legs = {}
+    for leg, kname in TX_LEGS.items():
+        f, w = pmc("fetch", kname), pmc("write", kname)
+        if f is None or w is None:
+            continue
+        legs[leg] = {"kernel": kname, "fetch_size_kib": f, "write_size_kib": w,
+                     "hbm_read_bytes_corrected": f * 1024 * 2, "hbm_write_bytes": w * 1024,
+                     "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024}
+    res = {"engine_build": build, "legs": legs,
+           "kernel_stats": rows(os.path.join(prof, "trace_kernel_stats.csv"))}
+    os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: round(v["traffic_bytes_per_launch"]) for k, v in legs.items()}))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3])
+    if sys.argv[2] == "tx":
+        main_tx(sys.argv[1], sys.argv[3])
+    else:
+        main(sys.argv[1], int(sys.argv[2]), sys.argv[3])
