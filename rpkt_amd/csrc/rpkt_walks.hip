@@ -134,7 +134,8 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const uint32_t c = k * kWave + lane;
-            v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+            // records and option bytes are read once: non-temporal loads (-2.6 %)
+            v[k] = (c / 5 < nrec) ? __builtin_nontemporal_load(&in[c]) : u32x4{0u, 0u, 0u, 0u};
         }
         uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
 #pragma unroll
@@ -180,7 +181,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             fix |= (uint32_t)straddles(addr[k], fb) << k;
         }
 #pragma unroll
-        for (int k = 0; k < kOptChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+        for (int k = 0; k < kOptChunks; ++k) d[k] = load16_fast<2>(rs, addr[k]);
 #pragma unroll
         for (int k = 0; k < kOptChunks; ++k) {
             const int c = k * kWave + lane;

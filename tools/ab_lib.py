@@ -1,0 +1,103 @@
+"""A/B timing of two builds of librpkt_gpu.so in one process (development tool, runs
+on the GPU box): kernel-time differences of a few percent are below the box-to-box
+spread, so both builds are timed interleaved on the same batch and their outputs are
+compared byte for byte.
+
+Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|layers9|forward2|build2|parse2|parse3]
+                              [--rounds 5] [--launches 20]
+The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
+  python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def build_b(out_dir, extra):
+    from rpkt_amd import build
+    os.makedirs(out_dir, exist_ok=True)
+    flags = [build.HIPCC, "--offload-arch=" + build.ARCH, "-O3", "-std=c++17", "-fPIC",
+             '-DRPKT_SRC_HASH="ab"'] + list(extra)
+    objs = []
+    for f in build.GPU_SRC:
+        o = os.path.join(out_dir, os.path.basename(f).replace(".hip", ".o"))
+        subprocess.check_call(flags + ["-c", "-o", o, f])
+        objs.append(o)
+    lib = os.path.join(out_dir, "librpkt_gpu.so")
+    subprocess.check_call([build.HIPCC, "--offload-arch=" + build.ARCH, "-shared", "-fPIC",
+                           "-o", lib] + objs)
+    print(lib)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib_b", nargs="?")
+    ap.add_argument("--build", metavar="OUT_DIR")
+    ap.add_argument("--leg", default="opts5")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    args, extra = ap.parse_known_args()
+    if args.build:
+        return build_b(args.build, extra)
+
+    import numpy as np
+    import torch
+    from rpkt_amd import engine, gen
+    A = engine.lib()
+    B = ctypes.CDLL(os.path.abspath(args.lib_b))
+    mode, cfg = args.leg.rstrip("0123456789"), int(args.leg[len(args.leg.rstrip("0123456789")):])
+    hb = gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else gen.make_batch(cfg)
+    db = engine.DeviceBatch.from_host(hb)
+    desc = db.desc()
+    recs = engine.parse_batch(db, 3)
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    P = ctypes.POINTER(engine.Batch)
+    outs, call = {}, {}
+    for name, L in (("A", A), ("B", B)):
+        if mode == "opts":
+            L.rpkt_gpu_options_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
+            call[name] = (lambda L=L, out=out: L.rpkt_gpu_options_batch(
+                ctypes.byref(desc), recs.data_ptr(), out.data_ptr(), sp))
+        elif mode == "layers":
+            L.rpkt_gpu_layers_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p]
+            out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
+            call[name] = (lambda L=L, out=out: L.rpkt_gpu_layers_batch(
+                ctypes.byref(desc), out.data_ptr(), sp))
+        elif mode == "parse":
+            L.rpkt_gpu_parse_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_uint32, ctypes.c_void_p]
+            out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
+            flags = 1 if cfg == 2 else 3
+            call[name] = (lambda L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
+                ctypes.byref(desc), flags, out.data_ptr(), None, 0, sp))
+        else:
+            raise SystemExit("leg %s: not wired (opts / layers / parse)" % args.leg)
+        outs[name] = out
+    times = {"A": [], "B": []}
+    for rnd in range(args.rounds + 1):
+        for name in ("A", "B"):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.launches):
+                rc = call[name]()
+                assert rc == 0, rc
+            e1.record(st)
+            torch.cuda.synchronize()
+            if rnd:
+                times[name].append(e0.elapsed_time(e1) / args.launches * 1e3)
+    same = outs["A"].cpu().numpy().tobytes() == outs["B"].cpu().numpy().tobytes()
+    print(json.dumps({"leg": args.leg, "n": hb.n, "identical": same,
+                      "A_us": round(float(np.median(times["A"])), 2),
+                      "B_us": round(float(np.median(times["B"])), 2)}))
+
+
+if __name__ == "__main__":
+    main()
