@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|layers9|forward2|build2|parse2|parse3]
+Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|layers9|forward2|build2|build3|parse2|parse3]
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -59,7 +59,12 @@ def main():
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
     P = ctypes.POINTER(engine.Batch)
-    outs, call = {}, {}
+    outs, call, keep_alive = {}, {}, []
+    forbid = engine.forbid_list([0xAC4A0001 + k for k in range(8)])
+    fwd = engine.Fwd()
+    fwd.dmac[:] = [0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]
+    fwd.smac[:] = [0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6]
+    fwd.forbid_dev, fwd.n_forbid = forbid.data_ptr(), forbid.numel()
     for name, L in (("A", A), ("B", B)):
         if mode == "opts":
             L.rpkt_gpu_options_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -78,8 +83,24 @@ def main():
             flags = 1 if cfg == 2 else 3
             call[name] = (lambda L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
                 ctypes.byref(desc), flags, out.data_ptr(), None, 0, sp))
+        elif mode in ("build", "forward"):          # in place: each side its own frames
+            dbx = engine.DeviceBatch.from_host(hb)
+            dx = dbx.desc()
+            out = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
+            keep_alive.append((dbx, dx))
+            if mode == "build":
+                L.rpkt_gpu_build_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_uint32,
+                                                   ctypes.c_void_p, ctypes.c_void_p]
+                call[name] = (lambda L=L, out=out, dx=dx: L.rpkt_gpu_build_batch(
+                    ctypes.byref(dx), recs.data_ptr(), 3, out.data_ptr(), sp))
+            else:
+                L.rpkt_gpu_forward_batch.argtypes = [P, ctypes.POINTER(engine.Fwd), ctypes.c_void_p,
+                                                     ctypes.c_void_p]
+                call[name] = (lambda L=L, out=out, dx=dx: L.rpkt_gpu_forward_batch(
+                    ctypes.byref(dx), ctypes.byref(fwd), out.data_ptr(), sp))
+            outs[name + "_frames"] = dbx.frames
         else:
-            raise SystemExit("leg %s: not wired (opts / layers / parse)" % args.leg)
+            raise SystemExit("leg %s: not wired" % args.leg)
         outs[name] = out
     times = {"A": [], "B": []}
     for rnd in range(args.rounds + 1):
@@ -93,7 +114,8 @@ def main():
             torch.cuda.synchronize()
             if rnd:
                 times[name].append(e0.elapsed_time(e1) / args.launches * 1e3)
-    same = outs["A"].cpu().numpy().tobytes() == outs["B"].cpu().numpy().tobytes()
+    same = all(outs[k].cpu().numpy().tobytes() == outs["B" + k[1:]].cpu().numpy().tobytes()
+               for k in outs if k.startswith("A"))
     print(json.dumps({"leg": args.leg, "n": hb.n, "identical": same,
                       "A_us": round(float(np.median(times["A"])), 2),
                       "B_us": round(float(np.median(times["B"])), 2)}))
