@@ -1,0 +1,21 @@
+#!/bin/bash
+# Turn a scripts/refresh_profiles.sh run (gpurun_out/prof_*) into the committed
+# summaries under profiles/: traffic_c<cfg>.json / traffic_tx.json (read by bench.py)
+# and per-profile trace stats, per-kernel PMC averages and bench logs.  Host side.
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+G=$R/gpurun_out
+for t in c2 c3 c4 c5 c7 walks; do
+    P=$G/prof_$t; D=$R/profiles/r01_$t
+    mkdir -p "$D"
+    cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
+    for k in fetch write; do
+        [ -f "$P/${k}_bench.log" ] && cp "$P/${k}_bench.log" "$D/"
+        python3 "$R/tools/pmc_by_kernel.py" "$P/${k}_counter_collection.csv" > "$D/${k}_by_kernel.json"
+    done
+    if [ "$t" = walks ]; then
+        python3 "$R/tools/traffic.py" "$P" tx "$R/profiles/traffic_tx.json"
+    else
+        python3 "$R/tools/traffic.py" "$P" "${t#c}" "$R/profiles/traffic_$t.json"
+    fi
+done

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Refresh every rocprofv3 trace + PMC traffic summary the bench line cites, for the
+# current engine build (GPU box).  Stops at the first failing pass.
+#   bash scripts/refresh_profiles.sh        -> gpurun_out/prof_{c2,c3,c4,c5,c7,walks}
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+for c in 2 3 4 5 7; do
+    bash "$R/scripts/profile.sh" "c$c" "$c"
+done
+bash "$R/scripts/profile.sh" walks 2 --tx layers9,opts5,forward2,build2
