@@ -32,7 +32,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from rpkt_amd import dist as rdist, engine, gen  # noqa: E402
+from rpkt_amd import dist as rdist, engine, fields, gen  # noqa: E402
 from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
@@ -347,6 +347,16 @@ def ip_u32(s):
     return (a << 24) | (b << 16) | (c << 8) | d
 
 
+# The fields leg's requests: the getters a receive loop reads on the capture mix.
+FIELD_LEG = [("ETHER_ETHERFRAME", "dst_addr"), ("ETHER_ETHERFRAME", "src_addr"),
+             ("ETHER_ETHERFRAME", "ethertype"), ("VLAN_VLANFRAME", "vlan_id"),
+             ("IPV4_IPV4", "src_addr"), ("IPV4_IPV4", "dst_addr"), ("IPV4_IPV4", "ttl"),
+             ("IPV4_IPV4", "protocol"), ("IPV6_IPV6", "src_addr", 0, "hi"),
+             ("IPV6_IPV6", "src_addr", 0, "lo"), ("IPV6_IPV6", "flow_label"),
+             ("IPV6_IPV6", "next_header"), ("UDP_UDP", "src_port"), ("UDP_UDP", "dst_port"),
+             ("TCP_TCP", "seq_num"), ("VXLAN_VXLAN", "vni")]
+
+
 def run_tx(cfg, mode, args, rank, world):
     """TX side: rpkt_gpu_build_batch (headers + both checksums filled, the
     rpkt_build.rs path) or rpkt_gpu_forward_batch (loopback_rx rewrite) over a
@@ -367,6 +377,12 @@ def run_tx(cfg, mode, args, rank, world):
     recs = [engine.parse_batch(db, 3) for db in dbs]
     outs = [torch.empty(hb.n * (64 if mode in ("opts", "layers") else 1), dtype=torch.uint8,
                         device="cuda") for hb in hbs]
+    if mode == "fields":                       # the walk once, outside the timed region
+        lays = [engine.layers_batch(db) for db in dbs]
+        reqs = fields.requests(FIELD_LEG)
+        vals = [torch.empty((hb.n, len(FIELD_LEG)), dtype=torch.int64, device="cuda")
+                for hb in hbs]
+        pres = [torch.empty(hb.n, dtype=torch.int32, device="cuda") for hb in hbs]
     forbid = engine.forbid_list([ip_u32(x) for x in FORBID_IPS])
     dmac, smac = bytes([0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]), bytes([0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6])
     stream = torch.cuda.current_stream()
@@ -379,6 +395,9 @@ def run_tx(cfg, mode, args, rank, world):
             engine.options_batch(dbs[j], recs[j], opts=outs[j], stream=stream)
         elif mode == "layers":
             engine.layers_batch(dbs[j], out=outs[j], stream=stream)
+        elif mode == "fields":
+            engine.fields_batch(dbs[j], lays[j], reqs, values=vals[j], present=pres[j],
+                                stream=stream)
         else:
             engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
 
@@ -407,6 +426,12 @@ def run_tx(cfg, mode, args, rank, world):
     elif mode == "layers":                     # header bytes walked + 64 B out per frame
         lo = outs[0].cpu().numpy().view(LAYERS_DTYPE)
         alg = int(np.minimum(lo["payload_off"].astype(np.int64), lens).sum()) + hbs[0].n * 64
+    elif mode == "fields":                     # layer records + field bytes read, values written
+        pm = pres[0].cpu().numpy().view(np.uint32)
+        nbytes = [(int(q["bit_off"]) + int(q["bits"]) - 1) // 8 - int(q["bit_off"]) // 8 + 1
+                  for q in reqs]
+        got = sum(int(((pm >> r) & 1).sum()) * nb for r, nb in enumerate(nbytes))
+        alg = hbs[0].n * (64 + 8 * len(reqs) + 4) + got
     elif mode == "opts":                       # records + option slices read, 64 B written
         ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
@@ -430,6 +455,8 @@ def run_tx(cfg, mode, args, rank, world):
                      if mode == "opts" else
                      "layers: pktfmt-derived protocol walk (captures mix, fuzzed)"
                      if mode == "layers" else
+                     "fields: %d pktfmt getters per frame over the layer walk (captures mix)"
+                     % len(FIELD_LEG) if mode == "fields" else
                      "forward: loopback_rx firewall fused (parse + both sums, 8 forbidden "
                      "sources, swap + ttl-1 + MACs + checksum update)")}
 
@@ -446,7 +473,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tx", default="build2,build3,forward2,opts5,layers9",
+    ap.add_argument("--tx", default="build2,build3,forward2,opts5,layers9,fields9",
                     help="legs beyond the parse reported under 'extra' (build<cfg>, "
                          "forward<cfg>, opts<cfg>)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
@@ -471,7 +498,7 @@ def main():
         if c != args.config:
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
     for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
-        mode = next(m for m in ("build", "forward", "opts", "layers") if leg.startswith(m))
+        mode = next(m for m in ("build", "forward", "opts", "layers", "fields") if leg.startswith(m))
         extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
 
     if rank == 0:

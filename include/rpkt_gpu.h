@@ -378,6 +378,41 @@ typedef struct rpkt_layers {
 /* layers_dev n * 64 B, 16-byte aligned. */
 int rpkt_gpu_layers_batch(const rpkt_batch_t* batch, rpkt_layers_t* layers_dev, void* stream);
 
+/* ---- Field getters over the layer walk ---------------------------------------------- */
+
+/* The header-field getters rpkt generates for every protocol of the walk
+ * (pktfmt/src/codegen/field.rs:115-250, `read_repr` / `read_multi_bytes`): a field of
+ * `bits` bits at bit `bit_off` of the protocol's header is the big-endian integer of
+ * bytes [bit_off/8, (bit_off+bits-1)/8], shifted right by 7 - (end bit in its byte)
+ * and masked to `bits` bits.  Byte-slice fields (MAC, IPv6 addresses) are
+ * byte-aligned: a request of up to 64 bits of one returns those bytes as a big-endian
+ * integer (ask for a 128-bit address as two 64-bit halves).  Offsets and widths per
+ * field come from the same specs (rpkt_amd/proto_fields.json).
+ *
+ * Request r of frame i reads the `nth` (0 = outermost) layer k of rpkt_layers_t i
+ * whose proto[k] == proto.  values_dev[i * n_req + r] is the field, or 0 when the
+ * frame has no such layer or the field's bytes pass the frame's end; bit r of
+ * present_dev[i] (optional, may be NULL) says which.  Replaces, per frame, the
+ * getter calls a receive loop makes on the header views it parsed, e.g.
+ * Ipv6::src_addr (ipv6/generated.rs), Arp::operation, Vxlan::vni, Gtpv1::teid. */
+typedef struct rpkt_field_req {
+    uint8_t  proto;      /* RPKT_P_*                                             */
+    uint8_t  nth;        /* occurrence of proto in the stack, 0 = outermost      */
+    uint8_t  bits;       /* 1..64                                                */
+    uint8_t  reserved;   /* 0                                                    */
+    uint16_t bit_off;    /* from the start of the protocol's header              */
+    uint16_t reserved2;  /* 0                                                    */
+} rpkt_field_req_t;
+
+#define RPKT_MAX_FIELD_REQS 32
+
+/* reqs: host memory, n_req in 1..RPKT_MAX_FIELD_REQS; layers_dev from
+ * rpkt_gpu_layers_batch on the same batch; values_dev n * n_req * 8 B, 8-B aligned;
+ * present_dev n * 4 B or NULL. */
+int rpkt_gpu_fields_batch(const rpkt_batch_t* batch, const rpkt_layers_t* layers_dev,
+                          const rpkt_field_req_t* reqs, uint32_t n_req, uint64_t* values_dev,
+                          uint32_t* present_dev, void* stream);
+
 /* 5-tuple hash used for flow buckets (host copy of the device function). */
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t src_port,
                         uint16_t dst_port, uint8_t protocol);

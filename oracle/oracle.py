@@ -80,6 +80,11 @@ def lib():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_void_p]
         L.oracle_layers_batch.restype = None
+        L.oracle_fields_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                          ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_fields_batch.restype = None
         _lib = L
     return _lib
 
@@ -207,6 +212,20 @@ def layers_batch(frames, n, offsets=None, stride=0, frame_len=0):
     lib().oracle_layers_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
                               _ptr(out))
     return out
+
+
+def fields_batch(frames, n, layers, reqs, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_fields_batch on the CPU: (values n x n_req uint64, present n uint32)."""
+    from rpkt_amd.records import FIELD_REQ_DTYPE, LAYERS_DTYPE
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    layers = np.ascontiguousarray(layers, dtype=LAYERS_DTYPE)
+    reqs = np.ascontiguousarray(reqs, dtype=FIELD_REQ_DTYPE)
+    values = np.zeros((n, reqs.size), dtype=np.uint64)
+    present = np.zeros(n, dtype=np.uint32)
+    lib().oracle_fields_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
+                              _ptr(layers), _ptr(reqs), reqs.size, _ptr(values), _ptr(present))
+    return values, present
 
 
 def flow_count(ev, n_buckets):

@@ -18,7 +18,7 @@ GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
 # the engine: one translation unit per kernel family, shared device code in rpkt_common.h
 GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
-           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_abi.hip")]
+           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_abi.hip")]
 GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]

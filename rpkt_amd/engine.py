@@ -48,7 +48,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
-           "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch"]
+           "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch"]
 
 _lib = None
 
@@ -106,6 +106,10 @@ def lib():
         L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.rpkt_gpu_layers_batch.restype = ctypes.c_int
+        L.rpkt_gpu_fields_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_fields_batch.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -344,3 +348,28 @@ def layers_batch(batch, out=None, stream=None):
     rc = lib().rpkt_gpu_layers_batch(ctypes.byref(d), out.data_ptr(), _stream_ptr(stream))
     _check(rc, "rpkt_gpu_layers_batch")
     return out
+
+
+def fields_batch(batch, layers, reqs, values=None, present=None, stream=None):
+    """rpkt_gpu_fields_batch: header-field getters over the layer walk.  `layers` is
+    rpkt_gpu_layers_batch's output on the same batch, `reqs` a FIELD_REQ_DTYPE array
+    (rpkt_amd.fields.requests builds one by protocol and field name).  Returns
+    (values: int64 tensor n x n_req holding the u64 bits, present: int32 tensor n,
+    bit r = request r)."""
+    import numpy as np
+    from .records import FIELD_REQ_DTYPE
+    torch = _torch()
+    reqs = np.ascontiguousarray(reqs, dtype=FIELD_REQ_DTYPE)
+    k = int(reqs.size)
+    dev = batch.frames.device
+    if values is None:
+        values = torch.empty((batch.n, k), dtype=torch.int64, device=dev)   # u64 bits
+    if present is None:
+        present = torch.empty(batch.n, dtype=torch.int32, device=dev)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_fields_batch(ctypes.byref(d), layers.data_ptr(),
+                                     reqs.ctypes.data_as(ctypes.c_void_p), k,
+                                     values.data_ptr(), present.data_ptr(),
+                                     _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_fields_batch")
+    return values, present

@@ -62,6 +62,13 @@ LAYERS_DTYPE = np.dtype([        # rpkt_layers_t (include/rpkt_gpu.h), 64 B
 assert LAYERS_DTYPE.itemsize == LAYERS_BYTES
 LAYER_STOP = {"END": 1, "UNKNOWN": 2, "ERR": 3, "MAX": 4}
 
+FIELD_REQ_DTYPE = np.dtype([      # rpkt_field_req_t (include/rpkt_gpu.h), 8 B
+    ("proto", "u1"), ("nth", "u1"), ("bits", "u1"), ("reserved", "u1"),
+    ("bit_off", "<u2"), ("reserved2", "<u2"),
+])
+assert FIELD_REQ_DTYPE.itemsize == 8
+MAX_FIELD_REQS = 32
+
 
 def protocol_names():
     """Protocol id -> name, from include/rpkt_protocols.h."""

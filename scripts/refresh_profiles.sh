@@ -7,4 +7,4 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 for c in 2 3 4 5 7; do
     bash "$R/scripts/profile.sh" "c$c" "$c"
 done
-bash "$R/scripts/profile.sh" walks 2 --tx layers9,opts5,forward2,build2
+bash "$R/scripts/profile.sh" walks 2 --tx layers9,opts5,forward2,build2,fields9

@@ -187,7 +187,8 @@ def build(ref):
             hl, pl = parse_length(body, fields)
             ent = {"id": len(packets), "spec": spec, "name": name, "hdr": hdr,
                    "hl_kind": 0, "hl": None, "hl_fixed": None, "pl_kind": 0, "pl": None,
-                   "cond": parse_cond(body, fields)}
+                   "cond": parse_cond(body, fields),
+                   "fields": {k: [v["off"], v["bits"]] for k, v in fields.items()}}
             if hl and hl[0] == "custom":
                 ent["hl_kind"] = 1 + CUSTOM_HL[name]
             elif hl:
@@ -366,6 +367,10 @@ def main(ref="/root/reference"):
         g.pop("key", None)
     for p in t["packets"]:
         p.pop("member", None)
+    with open(os.path.join(ROOT, "rpkt_amd", "proto_fields.json"), "w") as fh:
+        json.dump({"%s_%s" % (p["spec"].upper(), p["name"].upper()):
+                   {"id": p["id"], "hdr": p["hdr"], "fields": p["fields"]}
+                   for p in t["packets"]}, fh, indent=1)
     with open(os.path.join(ROOT, "tests", "golden", "proto_table.json"), "w") as fh:
         json.dump(t, fh, indent=1)
     print("%d packets in %d groups" % (len(t["packets"]), len(t["groups"])))

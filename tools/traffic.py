@@ -58,7 +58,7 @@ def main(prof, cfg, out):
 
 
 TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "options_kernel",
-           "layers9": "layers_kernel"}
+           "layers9": "layers_kernel", "fields9": "fields_kernel"}
 
 
 def main_tx(prof, out):
