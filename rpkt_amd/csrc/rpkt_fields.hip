@@ -6,15 +6,15 @@
 // (protocol, occurrence, bit offset, width) requests over every frame of a batch,
 // on the layer offsets rpkt_gpu_layers_batch found.
 //
-// One lane per (frame, request) output element, so the values are stored as one
-// contiguous 8-B-per-lane row per wave; the n_req lanes of a frame read the same
-// 64-B layer record and header bytes, which L1/L2 serve after the first lane.  The
-// gather is a handful of byte loads per lane: latency-bound, not HBM-bound.
+// One lane per frame (its 64-B layer record read once, the requests four at a time),
+// values staged through LDS and stored as contiguous rows.  A field is three aligned
+// dword loads and a funnel shift; the gather touches one or two lines per layer a request
+// names, so the kernel is latency-bound on those loads, not HBM-bound.
 #include "rpkt_common.h"
 
 namespace {
 
-constexpr int kFieldBlock = 256;
+constexpr int kFieldBlock = 128;            // LDS stage <= 128 * 65 * 4 = 33 KB
 
 struct FieldReqs {
     rpkt_field_req_t r[RPKT_MAX_FIELD_REQS];
@@ -56,47 +56,89 @@ __device__ __forceinline__ bool find_layer(const LayerView& L, uint32_t proto, u
     return found != 0;
 }
 
+// Bytes [a, a+9) of the batch, as (big-endian first 8, ninth), from the three aligned
+// dwords d[0..2] at a & ~3: a funnel shift and a byte swap.  Bytes past the field are
+// the frame's (or the next frame's) and are shifted out by the caller.
+__device__ __forceinline__ void take9(const uint32_t (&d)[3], uint32_t a, uint64_t& hi,
+                                      uint32_t& ninth) {
+    const uint32_t sh = 8u * (a & 3u);
+    uint64_t q = ((uint64_t)d[1] << 32) | d[0];
+    q = sh ? (q >> sh) | ((uint64_t)d[2] << (64u - sh)) : q;
+    hi = __builtin_bswap64(q);
+    ninth = (d[2] >> sh) & 0xffu;
+}
+
+// The same bytes by byte loads (bytes at or past `limit` read 0): for the rare field
+// in the last, partial dword of the buffer, which a dword load drops whole.
+__device__ __noinline__ void load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t limit,
+                                         uint64_t& hi, uint32_t& ninth) {
+    uint64_t h = 0;
+    for (uint32_t j = 0; j < 8; ++j) h = (h << 8) | (a + j < limit ? gbyte(rs, a + j) : 0u);
+    hi = h;
+    ninth = a + 8 < limit ? gbyte(rs, a + 8) : 0u;
+}
+
+constexpr uint32_t kReqGroup = 4;      // requests whose loads are in flight together
+
+// One lane per frame: its layer record once, then the requests in groups of four whose
+// twelve dword loads are issued before any is used (the request list is wave-uniform,
+// read from the kernel arguments by scalar loads; the host pads it to a multiple of
+// four with requests no layer matches).  Values are staged in LDS (frame stride
+// 2k+1 dwords: conflict-free) and stored as contiguous 8-B-per-lane rows of the
+// block's n_req x 128 outputs.
 __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
     const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len, uint32_t n,
     const rpkt_layers_t* __restrict__ layers, FieldReqs reqs, uint32_t n_req,
     uint64_t* __restrict__ values, uint32_t* __restrict__ present) {
-    const uint64_t e = (uint64_t)blockIdx.x * kFieldBlock + threadIdx.x;
-    if (e >= (uint64_t)n * n_req) return;
-    const uint32_t i = (uint32_t)(e / n_req), r = (uint32_t)(e - (uint64_t)i * n_req);
-    const Frame fr = frame_span(offsets, stride, frame_len, frames_bytes, i);
-    const LayerView L = load_layers(layers, i);
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
-
-    const rpkt_field_req_t q = reqs.r[r];
-    const uint32_t bit_off = q.bit_off, bits = q.bits;
-    const uint32_t sb = bit_off >> 3, eb = (bit_off + bits - 1) >> 3;
-    uint32_t loff;
-    const bool ok = find_layer(L, q.proto, q.nth, loff) && loff + eb < fr.len;
-    uint64_t v = 0;
-    if (ok) {
-        const uint32_t a = fr.off + loff + sb, nb = eb - sb + 1;   // 1..9 bytes
-        uint64_t hi = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            if (j < nb) hi |= (uint64_t)gbyte(rs, a + j) << (56 - 8 * j);
-        const uint32_t s = bit_off & 7u;
-        const uint32_t lo = nb == 9 ? gbyte(rs, a + 8) : 0u;
-        // the 64 bits from the field's first bit on, then the field's top `bits`
-        const uint64_t w = s ? (hi << s) | (uint64_t)(lo >> (8 - s)) : hi;
-        v = w >> (64 - bits);
-    }
-    values[e] = v;
-
-    if (present && r == 0) {
+    extern __shared__ uint32_t stage[];                  // kFieldBlock * (2 n_req + 1)
+    const uint32_t base = blockIdx.x * kFieldBlock, t = threadIdx.x, i = base + t;
+    const uint32_t nf = min(n - base, (uint32_t)kFieldBlock), fs = 2 * n_req + 1;
+    const uint32_t full_dwords = frames_bytes & ~3u;
+    if (i < n) {
+        const Frame fr = frame_span(offsets, stride, frame_len, frames_bytes, i);
+        const LayerView L = load_layers(layers, i);
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
         uint32_t mask = 0;
-        for (uint32_t k = 0; k < n_req; ++k) {
-            const rpkt_field_req_t t = reqs.r[k];
-            uint32_t o;
-            const uint32_t end = ((uint32_t)t.bit_off + t.bits - 1) >> 3;
-            if (find_layer(L, t.proto, t.nth, o) && o + end < fr.len) mask |= 1u << k;
+        for (uint32_t r0 = 0; r0 < n_req; r0 += kReqGroup) {
+            uint32_t d[kReqGroup][3], a[kReqGroup], ok[kReqGroup];
+#pragma unroll
+            for (uint32_t j = 0; j < kReqGroup; ++j) {
+                const rpkt_field_req_t q = reqs.r[r0 + j];
+                const uint32_t eb = ((uint32_t)q.bit_off + q.bits - 1) >> 3;
+                uint32_t loff;
+                ok[j] = find_layer(L, q.proto, q.nth, loff) & (loff + eb < fr.len);
+                a[j] = ok[j] ? fr.off + loff + (q.bit_off >> 3) : 0u;
+                const uint32_t a4 = a[j] & ~3u;
+                d[j][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)a4, 0, 0);
+                d[j][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a4 + 4u), 0, 0);
+                d[j][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a4 + 8u), 0, 0);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kReqGroup; ++j) {
+                const rpkt_field_req_t q = reqs.r[r0 + j];
+                const uint32_t bits = q.bits, s = q.bit_off & 7u;
+                uint64_t hi;
+                uint32_t ninth;
+                take9(d[j], a[j], hi, ninth);
+                if (ok[j] && a[j] + 9u > full_dwords) load9_bytes(rs, a[j], frames_bytes, hi, ninth);
+                // the 64 bits from the field's first bit on, then its top `bits`
+                const uint64_t w = s ? (hi << s) | (uint64_t)(ninth >> (8 - s)) : hi;
+                const uint64_t v = ok[j] ? w >> ((64u - bits) & 63u) : 0ull;
+                mask |= ok[j] << (r0 + j);
+                if (r0 + j < n_req) {
+                    stage[t * fs + 2 * (r0 + j)] = (uint32_t)v;
+                    stage[t * fs + 2 * (r0 + j) + 1] = (uint32_t)(v >> 32);
+                }
+            }
         }
-        present[i] = mask;
+        if (present) present[i] = mask;
+    }
+    __syncthreads();
+    uint64_t* out = values + (uint64_t)base * n_req;
+    for (uint32_t e = t; e < nf * n_req; e += kFieldBlock) {
+        const uint32_t f = e / n_req, r = e - f * n_req;
+        out[e] = ((uint64_t)stage[f * fs + 2 * r + 1] << 32) | stage[f * fs + 2 * r];
     }
 }
 
@@ -110,6 +152,8 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
     if (!b || !layers_dev || !reqs || !values_dev) return RPKT_E_INVAL;
     if (n_req == 0 || n_req > RPKT_MAX_FIELD_REQS) return RPKT_E_INVAL;
     FieldReqs rq = {};
+    for (uint32_t k = 0; k < RPKT_MAX_FIELD_REQS; ++k)      // padding: matches no layer
+        rq.r[k] = rpkt_field_req_t{0xff, 0, 8, 0, 0, 0};
     for (uint32_t k = 0; k < n_req; ++k) {
         const rpkt_field_req_t& t = reqs[k];
         if (t.bits == 0 || t.bits > 64 || t.proto >= RPKT_N_PROTOCOLS) return RPKT_E_INVAL;
@@ -124,10 +168,9 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
         ((uintptr_t)present_dev & 3u) != 0)
         return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint64_t total = (uint64_t)b->n * n_req;
-    const uint64_t grid = (total + kFieldBlock - 1) / kFieldBlock;
-    if (grid > 0x7fffffffull) return RPKT_E_TOO_LARGE;
-    return launch(fields_kernel, dim3((uint32_t)grid), dim3(kFieldBlock), 0, (hipStream_t)stream,
+    const uint32_t grid = (b->n + kFieldBlock - 1) / kFieldBlock;
+    const size_t lds = (size_t)kFieldBlock * (2 * n_req + 1) * 4;
+    return launch(fields_kernel, dim3(grid), dim3(kFieldBlock), lds, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
                   layers_dev, rq, n_req, values_dev, present_dev);
 }

@@ -59,9 +59,9 @@ def test_fields_baseline_configs(torch, cfg):
     check(gen.make_batch(cfg, 1 << 18), [chunk])
 
 
-@pytest.mark.parametrize("n,k", [(1, 1), (3, 7), (257, 3), (1000, 32), (4097, 5)])
+@pytest.mark.parametrize("n,k", [(1, 1), (3, 7), (129, 3), (257, 3), (1000, 32), (4097, 5)])
 def test_fields_ragged_sizes(torch, n, k):
-    """n x n_req around the 256-lane block: no value or mask past n is written."""
+    """n x n_req around the 128-frame block: no value or mask past n is written."""
     hb = gen.make_mix(n, seed=n + k)
     chunk = all_requests()[0][:k]
     db = engine.DeviceBatch.from_host(hb)
