@@ -6,7 +6,7 @@
 // (protocol, occurrence, bit offset, width) requests over every frame of a batch,
 // on the layer offsets rpkt_gpu_layers_batch found.
 //
-// One lane per frame (its 64-B layer record read once, the requests four at a time),
+// One lane per frame (its 64-B layer record read once, the requests eight at a time),
 // values staged through LDS and stored as contiguous rows.  A field is three aligned
 // dword loads and a funnel shift; the gather touches one or two lines per layer a request
 // names, so the kernel is latency-bound on those loads, not HBM-bound.
@@ -78,12 +78,12 @@ __device__ __noinline__ void load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a, 
     ninth = a + 8 < limit ? gbyte(rs, a + 8) : 0u;
 }
 
-constexpr uint32_t kReqGroup = 4;      // requests whose loads are in flight together
+constexpr uint32_t kReqGroup = 8;      // requests whose loads are in flight together
 
-// One lane per frame: its layer record once, then the requests in groups of four whose
-// twelve dword loads are issued before any is used (the request list is wave-uniform,
+// One lane per frame: its layer record once, then the requests in groups of eight whose
+// 24 dword loads are issued before any is used (the request list is wave-uniform,
 // read from the kernel arguments by scalar loads; the host pads it to a multiple of
-// four with requests no layer matches).  Values are staged in LDS (frame stride
+// eight with requests no layer matches).  Values are staged in LDS (frame stride
 // 2k+1 dwords: conflict-free) and stored as contiguous 8-B-per-lane rows of the
 // block's n_req x 128 outputs.
 __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
