@@ -125,3 +125,44 @@ def test_protocol_ids_match_table():
     assert len(names) == len(t["packets"])
     for p in t["packets"]:
         assert names[p["id"]] == ("%s_%s" % (p["spec"], p["name"])).upper()
+
+
+def test_field_req_layout_matches_header(tmp_path):
+    """offsetof() of rpkt_field_req_t, compiled from the header, against FIELD_REQ_DTYPE."""
+    import subprocess
+    names = records.FIELD_REQ_DTYPE.names
+    prog = ['#include <stdio.h>', '#include <stddef.h>', '#include "rpkt_gpu.h"',
+            'int main(void) { printf("%zu %d", sizeof(rpkt_field_req_t), RPKT_MAX_FIELD_REQS);']
+    prog += ['printf(" %%zu", offsetof(rpkt_field_req_t, %s));' % n for n in names]
+    prog += ['return 0; }']
+    src = tmp_path / "offs.c"
+    src.write_text("\n".join(prog))
+    exe = tmp_path / "offs"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HDR), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got[0] == records.FIELD_REQ_DTYPE.itemsize == 8
+    assert got[1] == records.MAX_FIELD_REQS
+    assert got[2:] == [records.FIELD_REQ_DTYPE.fields[n][1] for n in names]
+
+
+def test_fields_batch_argument_checks(L):
+    """Host-side validation of rpkt_gpu_fields_batch (returns before any device call)."""
+    import ctypes
+    import numpy as np
+    from rpkt_amd import fields
+    reqs = fields.requests([("IPV4_IPV4", "ttl")])
+    b = engine.Batch(frames_dev=16, frames_bytes=64, offsets_dev=None, stride=64,
+                     frame_len=64, n=0, reserved=0)
+    rp = reqs.ctypes.data_as(ctypes.c_void_p)
+    assert L.rpkt_gpu_fields_batch(None, 16, rp, 1, 16, None, None) == -1
+    assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 16, rp, 0, 16, None, None) == -1
+    assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 16, rp, 33, 16, None, None) == -1
+    assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 16, rp, 1, 16, None, None) == 0   # n == 0
+    for key, val in (("bits", 0), ("bits", 65), ("proto", 200)):
+        bad = reqs.copy()
+        bad[key] = val
+        assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 16, bad.ctypes.data_as(ctypes.c_void_p),
+                                       1, 16, None, None) == -1, (key, val)
+    b.n = 4
+    assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 8, rp, 1, 16, None, None) == -4  # align
+    assert np.asarray(reqs).size == 1
