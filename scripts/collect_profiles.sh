@@ -5,7 +5,7 @@
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
-for t in c2 c3 c4 c5 c7 walks; do
+for t in ${TAGS:-c2 c3 c4 c5 c7 walks build3}; do
     P=$G/prof_$t; D=$R/profiles/r01_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
@@ -13,7 +13,9 @@ for t in c2 c3 c4 c5 c7 walks; do
         [ -f "$P/${k}_bench.log" ] && cp "$P/${k}_bench.log" "$D/"
         python3 "$R/tools/pmc_by_kernel.py" "$P/${k}_counter_collection.csv" > "$D/${k}_by_kernel.json"
     done
-    if [ "$t" = walks ]; then
+    if [ "$t" = build3 ]; then
+        python3 "$R/tools/traffic.py" "$P" tx:build3 "$R/profiles/traffic_tx.json"
+    elif [ "$t" = walks ]; then
         python3 "$R/tools/traffic.py" "$P" tx "$R/profiles/traffic_tx.json"
     else
         python3 "$R/tools/traffic.py" "$P" "${t#c}" "$R/profiles/traffic_$t.json"

@@ -6,8 +6,10 @@ wide coalesced streaming read (MI355X_MICROARCH.md §HBM), so the read side is
 doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.
 Usage: python tools/traffic.py <prof_dir> <config> <out_json>
        python tools/traffic.py <prof_dir> tx <out_json>
-  (tx: a profile of `bench.py --tx build2,forward2,opts5,layers9`, one kernel per leg:
-   the TX and walk kernels' traffic per launch, keyed by bench leg)
+  (tx: a profile of `bench.py --tx build2,forward2,opts5,layers9,fields9`, one kernel
+   per leg: the TX and walk kernels' traffic per launch, keyed by bench leg)
+       python tools/traffic.py <prof_dir> tx:build3 <out_json>
+  (a profile of `bench.py --tx build3` alone, merged into out_json as leg build3)
 """
 import csv
 import json
@@ -61,7 +63,13 @@ TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "opt
            "layers9": "layers_kernel", "fields9": "fields_kernel"}
 
 
-def main_tx(prof, out):
+MODE_KERNEL = {"build": "build_kernel", "forward": "forward_kernel", "opts": "options_kernel",
+               "layers": "layers_kernel", "fields": "fields_kernel"}
+
+
+def main_tx(prof, out, only=None):
+    """All TX_LEGS of one profile, or (only = "build3") the one leg a profile of
+    `bench.py --tx build3` holds, merged into the existing summary of the same build."""
     def pmc(name, kname):
         v = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, name + "_counter_collection.csv"))
              if r["Kernel_Name"].startswith(kname)][5:]
@@ -73,7 +81,14 @@ def main_tx(prof, out):
             if line.startswith("{"):
                 build = json.loads(line).get("engine_build")
     legs = {}
-    for leg, kname in TX_LEGS.items():
+    if only:
+        with open(out) as fh:
+            old = json.load(fh)
+        assert old["engine_build"] == build, (old["engine_build"], build)
+        legs = old["legs"]
+    todo = TX_LEGS.items() if not only else \
+        [(only, next(k for m, k in MODE_KERNEL.items() if only.startswith(m)))]
+    for leg, kname in todo:
         f, w = pmc("fetch", kname), pmc("write", kname)
         if f is None or w is None:
             continue
@@ -82,6 +97,9 @@ def main_tx(prof, out):
                      "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024}
     res = {"engine_build": build, "legs": legs,
            "kernel_stats": rows(os.path.join(prof, "trace_kernel_stats.csv"))}
+    if only:
+        res["kernel_stats"] = old["kernel_stats"]
+        res.setdefault("kernel_stats_" + only, rows(os.path.join(prof, "trace_kernel_stats.csv")))
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
@@ -91,5 +109,7 @@ def main_tx(prof, out):
 if __name__ == "__main__":
     if sys.argv[2] == "tx":
         main_tx(sys.argv[1], sys.argv[3])
+    elif sys.argv[2].startswith("tx:"):
+        main_tx(sys.argv[1], sys.argv[3], only=sys.argv[2][3:])
     else:
         main(sys.argv[1], int(sys.argv[2]), sys.argv[3])
