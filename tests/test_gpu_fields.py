@@ -87,3 +87,31 @@ def test_fields_bad_requests(torch):
     bad["bits"], bad["proto"] = 8, 200
     with pytest.raises(engine.RpktError):
         engine.fields_batch(db, lay_d, bad)
+
+
+@pytest.mark.parametrize("lead", [0, 1, 2, 3])
+def test_fields_random_requests_past_frame_and_buffer_end(torch, lead):
+    """Random (protocol, nth, width, bit offset) requests, including fields that cross
+    the frame's end and, at the batch's last frame, the buffer's final partial dword
+    (frames_bytes = 4k + lead residue): the kernel's byte path."""
+    from test_oracle_fields import random_requests
+    rng = np.random.default_rng(100 + lead)
+    fr = gen.fixture_frames()
+    hb = host_batch(fr + fr[:3], lead)
+    check(hb, [random_requests(rng) for _ in range(8)])
+    # the batch's last frame ends at the buffer end, 4k + r bytes: Ethernet fields
+    # over its final bytes take the byte path of the buffer's last partial dword
+    base = lead + sum(len(f) for f in fr[:5]) + 23
+    last = fr[0][:23 + (lead - base) % 4]
+    hb = host_batch(fr[:5] + [last], lead)
+    assert hb.frames.size % 4 == lead
+    L = len(last)
+    chunk = [(0, 0, b, o) for b, o in zip([64, 33, 8, 1, 16, 57, 24, 40] * 4,
+                                          range(max(0, 8 * L - 96), 8 * L, 3))][:32]
+    check(hb, [chunk])
+    lay = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets)
+    _, pres = oracle.fields_batch(hb.frames, hb.n, lay, fields.requests(chunk),
+                                  offsets=hb.offsets)
+    assert pres[-1] != 0
+    hm = gen.make_mix(20000, seed=7 + lead)
+    check(hm, [random_requests(rng) for _ in range(4)])

@@ -139,3 +139,37 @@ def test_request_builder_rejects_bad_widths():
         fields.field("IPV4_IPV4", "ttl", 0, "hi")
     with pytest.raises(ValueError):
         fields.requests([("IPV4_IPV4", "ttl")] * 33)
+
+
+def random_requests(rng, k=32, max_bit=8 * 160):
+    """Requests past the fixed headers too: any protocol, bit offset and width, so
+    fields that cross or pass the frame's end (and the buffer's last dword) occur."""
+    names = list(fields.table())
+    out = []
+    for _ in range(k):
+        p = fields.table()[names[rng.integers(len(names))]]
+        out.append((p["id"], int(rng.integers(2)), int(rng.integers(1, 65)),
+                    int(rng.integers(0, max_bit))))
+    return out
+
+
+def test_oracle_matches_pktfmt_form_on_random_requests():
+    rng = np.random.default_rng(77)
+    hb = gen.make_mix(1500, seed=41)
+    lay = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets)
+    hits = misses = 0
+    for _ in range(6):
+        chunk = random_requests(rng)
+        v, pres = oracle.fields_batch(hb.frames, hb.n, lay, fields.requests(chunk),
+                                      offsets=hb.offsets)
+        for i in range(hb.n):
+            f = hb.frames[hb.offsets[i]:hb.offsets[i + 1]].tobytes()
+            L = lay[i]
+            for r, (pid, nth, bits, off) in enumerate(chunk):
+                ks = [k for k in range(L["n"]) if L["proto"][k] == pid]
+                ok = len(ks) > nth and int(L["off"][ks[nth]]) + (off + bits - 1) // 8 < len(f)
+                want = shift_mask(f[int(L["off"][ks[nth]]):], off, bits) if ok else 0
+                assert bool(pres[i] >> r & 1) == ok and int(v[i, r]) == want, (i, chunk[r])
+                hits += ok
+                misses += (len(ks) > nth) and not ok
+    assert hits > 1000 and misses > 1000
