@@ -37,23 +37,36 @@ __device__ __forceinline__ LayerView load_layers(const rpkt_layers_t* layers, ui
     return v;
 }
 
-// Offset of the nth layer whose protocol is `proto` (unrolled selects, no scratch
-// indexing); returns false when the stack has fewer such layers.
+// Offset of the nth layer whose protocol is `proto`; false when the stack has fewer
+// such layers.  Branch-free: a per-byte equality mask of the 16 protocol bytes (exact
+// zero-byte test on proto ^ layer bytes), cut to the n layers, then the nth set bit by
+// a 4-step popcount select, and the offset picked from the 8 offset dwords.
 __device__ __forceinline__ bool find_layer(const LayerView& L, uint32_t proto, uint32_t nth,
                                            uint32_t& loff) {
-    uint32_t seen = 0, found = 0, off = 0;
+    const uint32_t rep = proto * 0x01010101u;
+    uint32_t m = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < RPKT_MAX_LAYERS; ++k) {
-        const uint32_t p = (L.proto[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t o = (L.off[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        const uint32_t hit = (k < L.n) & (p == proto);
-        const uint32_t take = hit & (seen == nth) & (found ^ 1u);
-        off = take ? o : off;
-        found |= take;
-        seen += hit;
+    for (uint32_t w = 0; w < 4; ++w) {
+        const uint32_t x = L.proto[w] ^ rep;
+        const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+        m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u))
+             << (4 * w);
     }
-    loff = off;
-    return found != 0;
+    m &= 0xffffu >> (16u - min(L.n, (uint32_t)RPKT_MAX_LAYERS));
+    uint32_t pos = 0, r = nth, mm = m;
+#pragma unroll
+    for (uint32_t s = 8; s > 0; s >>= 1) {
+        const uint32_t c = __builtin_popcount(mm & ((1u << s) - 1u));
+        const bool skip = r >= c;
+        r = skip ? r - c : r;
+        mm = skip ? mm >> s : mm;
+        pos = skip ? pos + s : pos;
+    }
+    uint32_t dw = L.off[0];
+#pragma unroll
+    for (uint32_t q = 1; q < 8; ++q) dw = (pos >> 1) == q ? L.off[q] : dw;
+    loff = (dw >> (16 * (pos & 1))) & 0xffffu;
+    return (uint32_t)__builtin_popcount(m) > nth;
 }
 
 // Bytes [a, a+9) of the batch, as (big-endian first 8, ninth), from the three aligned
