@@ -6,8 +6,9 @@ frames, 1/2/4/8 MI355X.  One "step" = one rpkt_gpu_parse_batch launch over one
 synthetic batch already resident in HBM.
 
   headline  config 2: 1,048,576 x 64 B Ether/IPv4/UDP, stride 64, header extract +
-            IPv4 header sum.  Each rank rotates over 4 distinct batches so the
-            576 MiB working set is streamed from HBM, not the 256 MiB Infinity Cache.
+            IPv4 header sum.  Each rank rotates over 8 distinct batches, so the frames
+            alone (512 MiB, plus 640 MiB of records) are twice the 256 MiB Infinity
+            Cache and every launch streams its frames from HBM.
   also      config 3: 1,048,576 x 1500 B Ether/IPv4/TCP, full L3 + L4 sums
             (reported under "extra").
   --config 4: 8,388,608-frame IMIX sharded over the ranks (strong scaling) with
@@ -15,13 +16,21 @@ synthetic batch already resident in HBM.
   --config 7: 262,144 x 8000 B jumbo frames as mbuf chains (2048-B segments in
             shuffled 2176-B mempool slots), rpkt_gpu_parse_chains, full L3 + L4 sums.
 
-Multi-GPU: one process per GPU (torchrun); batches are independent, so ranks
-never exchange frames (weak scaling for configs 2/3).  The timed region is
-bracketed by barrier + synchronize and the max over ranks is reported.
+  config 1: benches/rpkt's packet_l4 over 1,000 x 64 B frames on the host CPU
+            (oracle restatement, 1 thread), ns/pkt under "extra".
+
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) this process is one
+rank; otherwise `--gpus N` (N > 1) starts the N rank processes itself, before any GPU
+call, and exits with their status.  Batches are independent, so ranks never exchange
+frames (weak scaling for configs 2/3); config 4 shards one batch and sums its flow
+counters with rpkt_gpu_flow_reduce (RCCL).  The timed region is bracketed by
+barrier + synchronize and the max over ranks is reported.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -62,10 +71,14 @@ def barrier(world):
         dist.barrier()
 
 
+def _red_device():
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
 def max_over_ranks(x, world):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -73,9 +86,56 @@ def max_over_ranks(x, world):
 def sum_over_ranks(x, world):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def usable_cpus():
+    """Host threads this process may run on: the affinity mask, capped by a cgroup v2
+    CPU quota when one is set (a GPU box grants a share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE + a local
+    rendezvous), wait for all of them and return the worst exit status.  Runs before
+    anything touches the GPU; the ranks are children, never an exec of this process."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    for q in procs:                 # one rank failed: the rest would hang
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
 
 
 def algorithmic_bytes(hb, flow=False):
@@ -194,68 +254,117 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline_chains(hc, gpu_recs, flags, seconds, max_bytes=256 << 20):
-    """Chain oracle (oracle/rpkt_oracle_chain.c, 1 thread) over the first chains of
-    the batch (~max_bytes of frame data); checks the GPU records of the sample."""
+_ORACLE_BUILD = None
+
+
+def oracle_for_baseline():
+    """The oracle, loaded from an -O3 -march=native build made on this host when gcc
+    is available, else from the shipped -march=x86-64-v3 build."""
+    global _ORACLE_BUILD
     from oracle import oracle
+    if _ORACLE_BUILD is None:
+        _ORACLE_BUILD = oracle.use_native_build() or "-O3 -march=x86-64-v3 (shipped build)"
+    return oracle, _ORACLE_BUILD
+
+
+def timed_reps(fn, seconds):
+    """Run fn() once to size the loop, then repeat it for >= `seconds`; returns
+    (reps, elapsed)."""
+    t0 = time.perf_counter()
+    fn()
+    one = time.perf_counter() - t0
+    reps = max(1, int(seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return reps, time.perf_counter() - t0
+
+
+def cpu_fields(value_mpps, gbs, threads, sample, reps, dt, build):
+    return {"value": round(value_mpps, 3), "unit": "Mpps", "cores": threads,
+            "gb_per_s": round(gbs, 3), "reps": reps, "seconds": round(dt, 2),
+            "sample": sample, "build": build}
+
+
+def cpu_baseline_chains(hc, gpu_recs, flags, seconds, threads_all, max_bytes=256 << 20):
+    """Chain oracle (oracle/rpkt_oracle_chain.c) over the first chains of the batch
+    (~max_bytes of frame data), 1 thread and all usable host threads, each for
+    >= `seconds`; checks the GPU records of the sample."""
+    oracle, build = oracle_for_baseline()
     m = int(np.searchsorted(np.cumsum(hc.lens()), max_bytes))
     m = max(1, min(m, hc.n))
     first = hc.chain_first[:m + 1]
     segs = hc.segs[:int(first[-1])]
-    t0 = time.perf_counter()
     o = oracle.parse_chains(hc.buf, segs, first, flags)
-    one = time.perf_counter() - t0
-    reps = max(1, int(seconds / max(one, 1e-6)))
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        oracle.parse_chains(hc.buf, segs, first, flags)
-    dt = time.perf_counter() - t0
     nbytes = int(hc.lens()[:m].sum())
-    return {
-        "value": round(m * reps / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
-        "cpu_model": cpu_model(),
-        "gb_per_s": round(nbytes * reps / dt / 1e9, 3),
-        "sample": "%d reps x first %d chains (%.0f MB, %d segments) of the batch, 1 thread, "
-                  "%.1f s" % (reps, m, nbytes / 1e6, segs.shape[0], dt),
-        "gpu_parity_on_sample": bool(gpu_recs[:m].tobytes() == o.tobytes()),
-    }
+    sample = "first %d chains (%.0f MB, %d segments) of the batch" % (m, nbytes / 1e6,
+                                                                       segs.shape[0])
+    reps, dt = timed_reps(lambda: oracle.parse_chains(hc.buf, segs, first, flags), seconds)
+    reps_a, dt_a = timed_reps(lambda: oracle.parse_chains(hc.buf, segs, first, flags,
+                                                          threads=threads_all), seconds)
+    out = cpu_fields(m * reps / dt / 1e6, nbytes * reps / dt / 1e9, 1,
+                     "%d reps x %s, 1 thread" % (reps, sample), reps, dt, build)
+    out.update(kind="port", cpu_model=cpu_model(), host_logical_cpus=os.cpu_count(),
+               all_cores=cpu_fields(m * reps_a / dt_a / 1e6, nbytes * reps_a / dt_a / 1e9,
+                                    threads_all, "%d reps x %s, %d threads (static partition)"
+                                    % (reps_a, sample, threads_all), reps_a, dt_a, build),
+               gpu_parity_on_sample=bool(gpu_recs[:m].tobytes() == o.tobytes()))
+    return out
 
 
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     """The CPU restatement of rpkt's path (oracle/, kind "port") timed on this host
-    over a bounded sample of the same workload; also checks the GPU records of the
-    sample bit-exact against it."""
-    from oracle import oracle
+    over a bounded sample of the same workload, 1 thread and all usable host threads,
+    each for >= `seconds`; also checks the GPU records of the sample bit-exact."""
+    oracle, build = oracle_for_baseline()
     hb = head_sample(hb)
     gpu_recs = gpu_recs[:hb.n]
     n = hb.n
+    nbytes = int(hb.lens().sum())
+
+    def run(threads):
+        return oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets,
+                                  stride=hb.stride, frame_len=hb.frame_len, threads=threads)
+    o = run(1)
+    sample = "first %d frames (%.0f MB) of the batch" % (n, nbytes / 1e6)
+    reps, dt = timed_reps(lambda: run(1), seconds)
+    reps_a, dt_a = timed_reps(lambda: run(threads_all), seconds)
+    out = cpu_fields(n * reps / dt / 1e6, nbytes * reps / dt / 1e9, 1,
+                     "%d reps x %s, 1 thread" % (reps, sample), reps, dt, build)
+    out.update(kind="port", cpu_model=cpu_model(), host_logical_cpus=os.cpu_count(),
+               all_cores=cpu_fields(n * reps_a / dt_a / 1e6, nbytes * reps_a / dt_a / 1e9,
+                                    threads_all, "%d reps x %s, %d threads (static partition)"
+                                    % (reps_a, sample, threads_all), reps_a, dt_a, build),
+               gpu_parity_on_sample=bool(gpu_recs.tobytes() == o.tobytes()))
+    return out
+
+
+def run_config1(args):
+    """Config 1 (BASELINE.json configs[0]): benches/rpkt's `packet_l4`
+    (rpkt_parse.rs:62-80) over 1,000 x 64 B Ether/IPv4/UDP frames built like
+    rpkt_build.rs:13-27, the oracle restatement on 1 host thread, >= cpu_seconds.
+    Reported in ns/pkt and Mpps like criterion would."""
+    oracle, build = oracle_for_baseline()
+    hb = gen.make_batch(1)
+    r = oracle.parse_batch(hb.frames, hb.n, flags=3, stride=hb.stride)
+    keys = ("ip_src", "ip_dst", "ip_checksum", "ip_ident", "src_port", "dst_port",
+            "l4_word6", "l4_checksum")
+    want = tuple(int(r[k][0]) for k in keys)
+    flen = hb.frame_len or hb.stride
+    bad = oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, flen, 1, want)
+    reps_probe = 1000
     t0 = time.perf_counter()
-    o = oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
-                           frame_len=hb.frame_len)
-    one = time.perf_counter() - t0
-    reps = max(1, int(seconds / max(one, 1e-6)))
+    oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, flen, reps_probe, want)
+    one = (time.perf_counter() - t0) / reps_probe
+    reps = max(1, int(args.cpu_seconds / max(one, 1e-9)))
     t0 = time.perf_counter()
-    for _ in range(reps):
-        oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
-                           frame_len=hb.frame_len)
+    bad += oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, flen, reps, want)
     dt = time.perf_counter() - t0
-    frames_total = n * reps
-    bytes_total = int(hb.lens().sum()) * reps
-    t0 = time.perf_counter()
-    oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
-                       frame_len=hb.frame_len, threads=threads_all)
-    dt_all = time.perf_counter() - t0
-    parity = gpu_recs.tobytes() == o.tobytes()
-    return {
-        "value": round(frames_total / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
-        "cpu_model": cpu_model(),
-        "gb_per_s": round(bytes_total / dt / 1e9, 3),
-        "sample": "%d reps x first %d frames (%.0f MB) of the batch, 1 thread, %.1f s" % (
-            reps, n, int(hb.lens().sum()) / 1e6, dt),
-        "all_cores": {"threads": threads_all,
-                      "value": round(n / dt_all / 1e6, 3), "unit": "Mpps"},
-        "gpu_parity_on_sample": bool(parity),
-    }
+    ns = dt / (reps * hb.n) * 1e9
+    return {"ns_per_pkt": round(ns, 3), "mpps": round(1e3 / ns, 2), "cores": 1,
+            "frames": hb.n, "frame_bytes": 64, "reps": reps, "seconds": round(dt, 2),
+            "asserts_failed": bad, "kind": "port", "build": build, "cpu_model": cpu_model(),
+            "what": "benches/rpkt packet_l4 (rpkt_parse.rs:62-80) restated in C, per frame"}
 
 
 def layout_name(hb):
@@ -279,7 +388,7 @@ def run_config(cfg, args, rank, world, cpu=False):
         scaling = "weak"
     else:                                          # weak scaling: a batch per rank
         n = args.frames or gen.DEFAULT_N[cfg]
-        R = args.rotate or (4 if cfg == 2 else 1)
+        R = args.rotate or (8 if cfg == 2 else 1)
         hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
                for r in range(R)]
         scaling = "weak"
@@ -319,18 +428,24 @@ def run_config(cfg, args, rank, world, cpu=False):
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
-        rdist.reduce_counters(flow["counters"])         # RCCL all-reduce over xGMI
+        try:
+            via = rdist.reduce_counters(flow["counters"], nb)    # rpkt_gpu_flow_reduce (RCCL)
+        except engine.RpktError as e:                  # nothing was enqueued: same sum via torch
+            dist.all_reduce(flow["counters"], op=dist.ReduceOp.SUM)
+            via = "torch.distributed all_reduce (C ABI reduce refused: %s)" % e
         torch.cuda.synchronize()
         red = time.perf_counter() - t0
         c = rdist.counters_as_u64(flow["counters"])
         out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
+        out["flow_reduce_via"] = via
         out["flow_pkts_total"] = int(c[:, 0].sum())
         # every launch (warmup included) added its shard's frames to the counters
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
     if cpu and rank == 0:
         g = as_records(recs[0].cpu().numpy())
         if cfg in gen.CHAINED:
-            out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds,
+                                                      args.cpu_threads)
         else:
             out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds,
                                                args.cpu_threads)
@@ -471,7 +586,8 @@ def main():
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="all-cores CPU leg threads (0 = every usable host thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--tx", default="build2,build3,forward2,opts5,layers9,fields9",
                     help="legs beyond the parse reported under 'extra' (build<cfg>, "
@@ -480,17 +596,45 @@ def main():
                     help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here (before any GPU call) and wait for them
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank, local, world = dist_env()
-    dev = local % torch.cuda.device_count() if args.dist_backend == "gloo" else local
+    if world != args.gpus:
+        print("[bench] error: %d rank(s) launched for --gpus %d" % (world, args.gpus),
+              file=sys.stderr)
+        sys.exit(3)
+    ndev = torch.cuda.device_count()                 # counts without initialising HIP
+    if args.dist_backend == "nccl" and local >= ndev:
+        print("[bench] error: rank %d needs cuda:%d but %d GPU(s) are visible (use "
+              "--dist-backend gloo to rehearse ranks on one GPU)" % (rank, local, ndev),
+              file=sys.stderr)
+        sys.exit(3)
+    dev = local % ndev if args.dist_backend == "gloo" else local
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
-            dist.init_process_group("gloo")
+            # gloo announces its peers on fd 1: keep stdout to the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
+        if dist.get_world_size() != args.gpus:
+            print("[bench] error: world size %d != --gpus %d" % (dist.get_world_size(),
+                                                                  args.gpus), file=sys.stderr)
+            sys.exit(3)
     want_cpu = (not args.no_cpu) and world == 1
+    if not args.cpu_threads:
+        args.cpu_threads = usable_cpus()
 
     main_res = run_config(args.config, args, rank, world, cpu=want_cpu)
     extra = {}
@@ -500,6 +644,8 @@ def main():
     for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
         mode = next(m for m in ("build", "forward", "opts", "layers", "fields") if leg.startswith(m))
         extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
+    if want_cpu and not args.no_config1:
+        extra["config1"] = run_config1(args)
 
     if rank == 0:
         fb = {2: 64, 3: 1500, 7: 8000}.get(args.config)
@@ -507,7 +653,7 @@ def main():
             "metric": METRIC,
             "value": round(main_res["mpps"], 2),
             "unit": "Mpps",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(main_res["ms_per_step"], 4),
@@ -520,7 +666,8 @@ def main():
                        main_res["frames_per_rank"], "frame_bytes": fb,
                        "layout": main_res["layout"], "checksums": main_res["flags"],
                        "parallelism": "replicas x%d (independent batches, no collective)" % world
-                       if args.config != 4 else "shard x%d + RCCL all-reduce" % world},
+                       if args.config != 4 else "shard x%d + RCCL all-reduce" % world,
+                       "dist_backend": args.dist_backend if world > 1 else None},
             "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
             "kernel_ms": round(main_res["kernel_ms"], 5),
             "warmup_launches": main_res["warmup_launches"],
@@ -530,7 +677,7 @@ def main():
             "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                           for kk, vv in v.items()} for k, v in extra.items()},
         }
-        for k in ("flow_reduce_ms", "flow_pkts_total", "flow_pkts_expected"):
+        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_pkts_total", "flow_pkts_expected"):
             if k in main_res:
                 line[k] = main_res[k]
         print(json.dumps(line), flush=True)

@@ -68,7 +68,8 @@ enum rpkt_err {
     RPKT_E_INVAL = -1,       /* NULL pointer / zero stride / bad flags            */
     RPKT_E_HIP = -2,         /* a HIP runtime call failed (see rpkt_gpu_last_hip_error) */
     RPKT_E_TOO_LARGE = -3,   /* frames_bytes >= 4 GiB: split the batch             */
-    RPKT_E_ALIGN = -4        /* out/flow buffer not 16-byte aligned               */
+    RPKT_E_ALIGN = -4,       /* out/flow buffer not 16-byte aligned               */
+    RPKT_E_COLL = -5         /* an RCCL call failed (see rpkt_gpu_last_coll_error) */
 };
 
 /* ---- flags for rpkt_gpu_parse_batch ---- */
@@ -195,6 +196,20 @@ size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets);
 int rpkt_gpu_flow_count(const rpkt_flow_ev_t* flow_ev_dev, uint32_t n,
                         uint32_t n_buckets, uint64_t* counters_dev,
                         void* workspace_dev, void* stream);
+
+/* Sum the flow counters of every rank (the path's only collective):
+ * one RCCL ncclAllReduce (root == -1) or ncclReduce to rank `root` of
+ * u64[(n_buckets+1)*4] in place, ncclUint64 / ncclSum, on `nccl_comm` (an
+ * ncclComm_t passed as void*) and `stream`.  Asynchronous like every call here.
+ * Replaces the per-queue counters a DPDK receive thread keeps and the final sum
+ * over threads (rpkt-dpdk/examples/loopback_tx.rs:176-181, rss_rx.rs:54-113).
+ * counters_dev 8-byte aligned.  RPKT_E_COLL: rpkt_gpu_last_coll_error() holds the
+ * ncclResult_t. */
+int rpkt_gpu_flow_reduce(uint64_t* counters_dev, uint32_t n_buckets, int root, void* nccl_comm,
+                         void* stream);
+/* Last ncclResult_t seen by this thread (0 if none); RCCL version (ncclGetVersion). */
+int rpkt_gpu_last_coll_error(void);
+int rpkt_gpu_coll_version(void);
 
 /* Batched checksum::from_slice over byte ranges of a device buffer:
  * out_dev[i] = from_slice(buf[start_i .. start_i + len_i]) for

@@ -11,8 +11,12 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "librpkt_oracle.so")
+NATIVE_LIB_PATH = os.path.join(HERE, "_build", "librpkt_oracle_native.so")
+ASAN_LIB_PATH = os.path.join(HERE, "_build", "librpkt_oracle_asan.so")
 
 _lib = None
+# RPKT_ORACLE_BUILD=asan: the sanitizer build (tests/test_oracle_asan.py sets it in a child)
+_lib_path = ASAN_LIB_PATH if os.environ.get("RPKT_ORACLE_BUILD") == "asan" else LIB_PATH
 
 
 def build():
@@ -20,12 +24,40 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+def use_native_build():
+    """Switch this process to an -O3 -march=native build of the oracle compiled on
+    the host it runs on (the CPU-baseline build SURVEY.md §8d names).  Must be
+    called before the first oracle call.  Returns the compiler flags used, or None
+    (and keeps the shipped x86-64-v3 build) when gcc fails here."""
+    global _lib_path
+    if _lib is not None:
+        raise RuntimeError("oracle already loaded from %s" % _lib_path)
+    try:
+        subprocess.check_call(["make", "-s", "-C", HERE, "native"], stdout=subprocess.DEVNULL)
+    except (OSError, subprocess.CalledProcessError):
+        return None
+    _lib_path = NATIVE_LIB_PATH
+    return "-O3 -march=native"
+
+
+def use_asan_build():
+    """Load the ASan/UBSan build instead (host sanitizer runs of the CPU tests; the
+    process must have libasan preloaded, see tests/test_oracle_asan.py)."""
+    global _lib_path
+    if _lib is not None:
+        raise RuntimeError("oracle already loaded from %s" % _lib_path)
+    subprocess.check_call(["make", "-s", "-C", HERE, "asan"], stdout=subprocess.DEVNULL)
+    _lib_path = ASAN_LIB_PATH
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if _lib_path == LIB_PATH and not os.path.exists(LIB_PATH):
             build()
-        L = ctypes.CDLL(LIB_PATH)
+        if _lib_path == ASAN_LIB_PATH and not os.path.exists(ASAN_LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", HERE, "asan"])
+        L = ctypes.CDLL(_lib_path)
         u8p = ctypes.POINTER(ctypes.c_uint8)
         L.oracle_from_slice.argtypes = [u8p, ctypes.c_size_t]
         L.oracle_from_slice.restype = ctypes.c_uint16
@@ -55,6 +87,17 @@ def lib():
                                        ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
                                        ctypes.c_uint16]
         L.oracle_packet_l4.restype = ctypes.c_int
+        L.oracle_packet_l4_loop.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint16,
+                                            ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
+                                            ctypes.c_uint16]
+        L.oracle_packet_l4_loop.restype = ctypes.c_uint64
+        L.oracle_parse_chains_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int]
+        L.oracle_parse_chains_mt.restype = ctypes.c_int
         L.oracle_parse_chains.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
@@ -138,7 +181,7 @@ def parse_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0, n_bucke
     return (recs, ev) if flow_ev else recs
 
 
-def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False):
+def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False, threads=1):
     """Oracle records for mbuf chains (rpkt_gpu_parse_chains arguments, host memory):
     segs = u32 (offset, length) pairs into buf, chain_first = n_chains + 1 entries."""
     from rpkt_amd.records import REC_DTYPE
@@ -148,9 +191,28 @@ def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False):
     n = cf.size - 1
     recs = np.zeros(n, dtype=REC_DTYPE)
     ev = np.zeros(n, dtype=np.uint64) if flow_ev else None
-    lib().oracle_parse_chains(_ptr(buf), buf.size, _ptr(segs), segs.size // 2, _ptr(cf), n,
-                              flags, n_buckets, _ptr(recs), _ptr(ev))
+    if threads > 1:
+        lib().oracle_parse_chains_mt(_ptr(buf), buf.size, _ptr(segs), segs.size // 2, _ptr(cf), n,
+                                     flags, n_buckets, _ptr(recs), _ptr(ev), threads)
+    else:
+        lib().oracle_parse_chains(_ptr(buf), buf.size, _ptr(segs), segs.size // 2, _ptr(cf), n,
+                                  flags, n_buckets, _ptr(recs), _ptr(ev))
     return (recs, ev) if flow_ev else recs
+
+
+def packet_l4(frame, want):
+    """benches/rpkt/rpkt_parse.rs:62-80 `packet_l4` on one frame: 0 when every assert
+    holds.  want = (src u32, dst u32, ip checksum, ident, sport, dport, udp length,
+    udp checksum)."""
+    b = np.ascontiguousarray(np.frombuffer(bytes(frame), dtype=np.uint8))
+    return int(lib().oracle_packet_l4(_ptr(b), b.size, *want))
+
+
+def packet_l4_loop(frames, n, stride, frame_len, reps, want):
+    """`reps` passes of packet_l4 over n frames at `stride` (config 1's timed loop, all in
+    C); returns the number of failed frames over all passes."""
+    f = np.ascontiguousarray(frames, dtype=np.uint8)
+    return int(lib().oracle_packet_l4_loop(_ptr(f), n, stride, frame_len, reps, *want))
 
 
 def pbuf_script(seg_lens, ops):

@@ -343,3 +343,21 @@ int oracle_packet_l4(const uint8_t* frame, uint32_t len, uint32_t want_src, uint
     if (r.l4_word6 != want_ulen || r.l4_checksum != want_udp_ck) return 5;
     return 0;
 }
+
+/* Config 1's timed loop: `reps` passes of packet_l4 over n frames at `stride`
+ * (criterion's b.iter body, benches/rpkt/rpkt_parse.rs:108-140, once per frame).
+ * Returns the number of frames whose asserts failed (summed over reps). */
+uint64_t oracle_packet_l4_loop(const uint8_t* frames, uint32_t n, uint32_t stride, uint32_t len,
+                               uint32_t reps, uint32_t want_src, uint32_t want_dst,
+                               uint16_t want_ip_ck, uint16_t want_ident, uint16_t want_sport,
+                               uint16_t want_dport, uint16_t want_ulen, uint16_t want_udp_ck) {
+    uint64_t bad = 0;
+    for (uint32_t r = 0; r < reps; r++)
+        for (uint32_t i = 0; i < n; i++) {
+            const uint8_t* f = frames + (size_t)i * stride;
+            __asm__ volatile("" : : "r"(f) : "memory");   /* no hoisting across reps */
+            bad += oracle_packet_l4(f, len, want_src, want_dst, want_ip_ck, want_ident,
+                                    want_sport, want_dport, want_ulen, want_udp_ck) != 0;
+        }
+    return bad;
+}

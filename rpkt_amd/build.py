@@ -1,6 +1,7 @@
 """Build the native libraries in-tree (they travel to the GPU box with the repo).
 
-  rpkt_amd/_build/librpkt_gpu.so   HIP engine for gfx950 + C ABI (include/rpkt_gpu.h)
+  rpkt_amd/_build/librpkt_gpu.so   HIP engine for gfx950 + C ABI (include/rpkt_gpu.h),
+                                   linked to RCCL for rpkt_gpu_flow_reduce
   rpkt_amd/_build/librpkt_gen.so   host C++ synthetic frame generator
 
 hipcc cross-compiles gfx950 without a GPU.  Rebuilds only when a source is newer.
@@ -13,12 +14,14 @@ ROOT = os.path.dirname(HERE)
 OUT = os.path.join(HERE, "_build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RPKT_OFFLOAD_ARCH", "gfx950")
+ROCM_LIB = "/opt/rocm/lib"
 
 GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
 # the engine: one translation unit per kernel family, shared device code in rpkt_common.h
 GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
-           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_abi.hip")]
+           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_abi.hip",
+            "rpkt_coll.hip")]
 GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
@@ -54,7 +57,9 @@ def build_gpu(force=False, extra=()):
     with ThreadPoolExecutor(max_workers=len(GPU_SRC)) as ex:
         list(ex.map(lambda so: subprocess.check_call(flags + ["-c", "-o", so[1], so[0]]),
                     zip(GPU_SRC, objs)))
-    subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", GPU_LIB] + objs)
+    # librccl.so.1 by soname: under torch it resolves to the RCCL torch already loaded
+    subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", GPU_LIB] + objs +
+                          ["-L" + ROCM_LIB, "-lrccl"])
     return GPU_LIB
 
 
@@ -67,17 +72,25 @@ def build_gen(force=False):
     return GEN_LIB
 
 
-EXAMPLE_SRC = os.path.join(ROOT, "examples", "parse_batch.cpp")
+EXAMPLES = ("parse_batch", "flow_reduce")
 EXAMPLE_BIN = os.path.join(ROOT, "examples", "parse_batch")
+FLOW_REDUCE_BIN = os.path.join(ROOT, "examples", "flow_reduce")
 
 
 def build_example(force=False):
-    """The C++ host example: links librpkt_gpu.so through the C ABI only."""
-    if force or _stale(EXAMPLE_BIN, [EXAMPLE_SRC, GPU_LIB] + HDR):
-        cmd = [HIPCC, "-O2", "-I" + os.path.join(ROOT, "include"), EXAMPLE_SRC, "-L" + OUT,
-               "-lrpkt_gpu", "-Wl,-rpath,$ORIGIN/../rpkt_amd/_build", "-o", EXAMPLE_BIN]
-        subprocess.check_call(cmd)
-    return EXAMPLE_BIN
+    """The C++ host examples: link librpkt_gpu.so through the C ABI only (and RCCL for
+    the communicator flow_reduce makes)."""
+    out = []
+    for name in EXAMPLES:
+        src = os.path.join(ROOT, "examples", name + ".cpp")
+        binp = os.path.join(ROOT, "examples", name)
+        if force or _stale(binp, [src, GPU_LIB] + HDR):
+            cmd = [HIPCC, "-O2", "-I" + os.path.join(ROOT, "include"), src, "-L" + OUT,
+                   "-lrpkt_gpu", "-L" + ROCM_LIB, "-lrccl",
+                   "-Wl,-rpath,$ORIGIN/../rpkt_amd/_build", "-o", binp]
+            subprocess.check_call(cmd)
+        out.append(binp)
+    return out
 
 
 def build_all(force=False):

@@ -14,7 +14,8 @@ from .build import GPU_LIB
 from .records import LAYERS_BYTES, OPTS_BYTES, REC_BYTES, F_FLOW_EV
 
 RPKT_OK = 0
-ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN"}
+ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN",
+          -5: "RPKT_E_COLL"}
 
 
 class RpktError(RuntimeError):
@@ -48,7 +49,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_flow_count", "rpkt_gpu_checksum_ranges", "rpkt_flow_hash",
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
-           "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch"]
+           "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch",
+           "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version"]
 
 _lib = None
 
@@ -110,6 +112,11 @@ def lib():
                                             ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_fields_batch.restype = ctypes.c_int
+        L.rpkt_gpu_flow_reduce.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_flow_reduce.restype = ctypes.c_int
+        L.rpkt_gpu_last_coll_error.restype = ctypes.c_int
+        L.rpkt_gpu_coll_version.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -128,6 +135,8 @@ def _check(rc, what):
         extra = ""
         if rc == -2:
             extra = " (hipError %d)" % lib().rpkt_gpu_last_hip_error()
+        elif rc == -5:
+            extra = " (ncclResult %d)" % lib().rpkt_gpu_last_coll_error()
         raise RpktError("%s failed: %s%s" % (what, ERRORS.get(rc, rc), extra))
 
 
@@ -211,6 +220,32 @@ def flow_count(flow_ev, n, n_buckets, counters=None, workspace=None, stream=None
                                    workspace.data_ptr(), _stream_ptr(stream))
     _check(rc, "rpkt_gpu_flow_count")
     return counters
+
+
+def flow_reduce(counters, n_buckets, comm, root=-1, stream=None):
+    """rpkt_gpu_flow_reduce: sum `counters` (u64[(n_buckets+1)*4] as int64) over every
+    rank of the RCCL communicator `comm` (an ncclComm_t as int, e.g. from
+    nccl_comm_of()), in place; root -1 = all-reduce, else reduce to that rank."""
+    if counters.numel() != (n_buckets + 1) * 4:
+        raise RpktError("counters must hold (n_buckets + 1) * 4 words")
+    rc = lib().rpkt_gpu_flow_reduce(counters.data_ptr(), n_buckets, root,
+                                    ctypes.c_void_p(int(comm)), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_flow_reduce")
+    return counters
+
+
+def nccl_comm_of(group=None):
+    """The ncclComm_t (as int) of torch.distributed's RCCL process group for the current
+    device, or None when the group's backend is not nccl (gloo rehearsals)."""
+    torch = _torch()
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    g = group if group is not None else dist.group.WORLD
+    if dist.get_backend(g) != "nccl":
+        return None
+    ptr = int(g._get_backend(torch.device("cuda", torch.cuda.current_device()))._comm_ptr())
+    return ptr or None
 
 
 def checksum_ranges(buf, ranges, out=None, stream=None):

@@ -106,7 +106,19 @@ def test_engine_refuses_cpu_fallback():
 
 def test_cpp_example_builds_against_header():
     from rpkt_amd.build import build_example
-    assert os.path.exists(build_example())
+    assert all(os.path.exists(p) for p in build_example())
+
+
+def test_flow_reduce_validation_without_launch(L):
+    """rpkt_gpu_flow_reduce's argument checks (no communicator is ever touched)."""
+    assert L.rpkt_gpu_flow_reduce(None, 8192, -1, 4096, None) == -1          # NULL counters
+    assert L.rpkt_gpu_flow_reduce(4096, 8192, -1, None, None) == -1          # NULL comm
+    assert L.rpkt_gpu_flow_reduce(4096, 0, -1, 4096, None) == -1             # no buckets
+    assert L.rpkt_gpu_flow_reduce(4096, 65536, -1, 4096, None) == -1         # too many
+    assert L.rpkt_gpu_flow_reduce(4096, 8192, -2, 4096, None) == -1          # bad root
+    assert L.rpkt_gpu_flow_reduce(4100, 8192, -1, 4096, None) == -4          # misaligned
+    assert L.rpkt_gpu_last_coll_error() == 0
+    assert L.rpkt_gpu_coll_version() >= 21000                                # RCCL 2.x
 
 
 def test_layers_layout_matches_header():

@@ -1,0 +1,127 @@
+"""Multi-rank paths on the GPU: ranks that each run the real HIP parse + flow-count on
+their shard and sum counters across ranks, the bench's own N-rank launcher, and the
+C ABI's RCCL reduce on torch.distributed's communicator.  The lease has one GPU, so
+the 2-rank cases share cuda:0 over gloo (RCCL refuses two ranks on one device); the
+RCCL call itself runs on a world-1 communicator here and on 8 GPUs in the driver's
+scaling run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 300000
+NB = 8192
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from rpkt_amd import dist as rd, engine, gen
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = rd.shard_range(N, rank, world)
+    hb = gen.make_batch(4, hi - lo, first=lo)
+    db = engine.DeviceBatch.from_host(hb)
+    _, ev = engine.parse_batch(db, 3 | 4, n_buckets=NB)
+    c = engine.flow_count(ev, hb.n, NB)
+    via = rd.reduce_counters(c, NB)
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.save(out, c.cpu().numpy())
+        with open(out + ".via", "w") as fh:
+            fh.write(via)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_hip_flow_counters_equal_whole_batch(tmp_path, world):
+    """Each rank: its shard of the config-4 IMIX batch through rpkt_gpu_parse_batch
+    (flow events) + rpkt_gpu_flow_count on cuda:0; counters summed over the ranks must
+    equal the oracle's counters of the whole batch, word for word."""
+    from oracle import oracle
+    from rpkt_amd import gen
+    out = str(tmp_path / "c.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out).view(np.uint64)
+    assert open(out + ".via").read() == "gloo"
+    hb = gen.make_batch(4, N)
+    _, ev = oracle.parse_batch(hb.frames, hb.n, flags=3, offsets=hb.offsets, n_buckets=NB,
+                               flow_ev=True, threads=8)
+    want = oracle.flow_count(ev, NB).reshape(-1, 4)
+    assert int(want[:, 0].sum()) == N
+    assert np.array_equal(got.reshape(-1, 4), want)
+
+
+def test_bench_launches_two_ranks():
+    """bench.py --gpus 2 starts its own two ranks (no torchrun), each parses its shard of
+    config 4 and the counter sum covers every frame of every launch of every rank."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--config", "4", "--also", "", "--tx", "",
+                        "--no-cpu", "--frames", "400000", "--steps", "3", "--warmup", "1",
+                        "--min-warmup-s", "0"], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "gloo"
+    assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
+    assert line["flow_reduce_via"] == "gloo"
+
+
+RCCL_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, %r)
+import numpy as np, torch, torch.distributed as dist
+from rpkt_amd import engine
+torch.cuda.set_device(0)
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=%r, RANK="0", WORLD_SIZE="1")
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+comm = engine.nccl_comm_of()
+assert comm, "no RCCL communicator"
+nb = 8192
+rng = np.random.default_rng(5)
+host = rng.integers(0, 2**62, (nb + 1) * 4, dtype=np.int64)
+c = torch.from_numpy(host.copy()).cuda()
+engine.flow_reduce(c, nb, comm)                    # all-reduce over the world-1 comm
+engine.flow_reduce(c, nb, comm, root=0)            # reduce to rank 0
+torch.cuda.synchronize()
+assert np.array_equal(c.cpu().numpy(), host)
+try:
+    engine.flow_reduce(c, nb, comm, root=1)        # no rank 1 in this world
+    raise SystemExit("root 1 accepted")
+except engine.RpktError:
+    pass
+print("rccl ok", engine.lib().rpkt_gpu_coll_version())
+dist.destroy_process_group()
+"""
+
+
+def test_flow_reduce_on_torch_rccl_communicator(tmp_path):
+    """rpkt_gpu_flow_reduce on the ncclComm_t of torch.distributed's RCCL group (the
+    communicator the bench's N-rank config 4 hands the C ABI)."""
+    script = tmp_path / "rccl.py"
+    script.write_text(RCCL_SCRIPT % (ROOT, str(_free_port())))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True,
+                       timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "rccl ok" in r.stdout

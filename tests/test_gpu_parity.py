@@ -257,10 +257,22 @@ def test_cpp_host_example_through_c_abi(torch):
     """examples/parse_batch: a non-Python host (plain hipMalloc) drives the C ABI."""
     import subprocess
     from rpkt_amd.build import build_example
-    exe = build_example()
+    exe = build_example()[0]
     r = subprocess.run([exe, "100000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "status=OK" in r.stdout and "sport=60376" in r.stdout
+
+
+def test_cpp_flow_reduce_through_c_abi(torch):
+    """examples/flow_reduce: a C++ host shards frames over the visible GPUs, parses with
+    flow events, counts, and sums the counters with rpkt_gpu_flow_reduce over an
+    ncclCommInitAll communicator; every counter word must equal the host's count."""
+    import subprocess
+    from rpkt_amd.build import FLOW_REDUCE_BIN
+    r = subprocess.run([FLOW_REDUCE_BIN, "300000", "8192"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "differing from the host count on any GPU: 0" in r.stdout, r.stdout
 
 
 def test_checksum_chains_match_from_buf(torch):

@@ -234,3 +234,15 @@ def test_chain_edge_cases():
     assert recs["status"].tolist() == [STATUS["ETH_SHORT"], STATUS["OK"], STATUS["OK"],
                                        STATUS["ETH_SHORT"]]
     assert recs["frame_len"].tolist() == [0, 1500, int(segs[1:, 1].sum()), 0]
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_chain_oracle_threads_partition(threads):
+    """The all-cores driver over chains (oracle_parse_chains_mt) equals the 1-thread walk,
+    flow events included."""
+    hc = gen.make_chains(8, 3001, seed=17)
+    one, e1 = oracle.parse_chains(hc.buf, hc.segs, hc.chain_first, 3, n_buckets=512,
+                                  flow_ev=True)
+    mt, e2 = oracle.parse_chains(hc.buf, hc.segs, hc.chain_first, 3, n_buckets=512,
+                                 flow_ev=True, threads=threads)
+    assert one.tobytes() == mt.tobytes() and np.array_equal(e1, e2)

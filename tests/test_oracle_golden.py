@@ -216,3 +216,41 @@ def test_views_vlan_group_parse_dot3():
     assert isinstance(vd, VlanDot3Frame) and vd.payload_len() == 357
     llc = vd.payload().chunk()
     assert (llc[0], llc[1], llc[2]) == (0xaa, 0xaa, 0x03)
+
+
+BENCH_WANT = ((192 << 24) | (168 << 16) | (29 << 8) | 58, (192 << 24) | (168 << 16) | (29 << 8) | 160,
+              0x0000, 0x5c65, 60376, 161, 74, 0xbc86)     # benches/rpkt/rpkt_parse.rs:62-80
+
+
+def test_packet_l4_on_bench_frame():
+    """Config 1's harness body (`packet_l4`, rpkt_parse.rs:62-80) holds on the reference's
+    own 110-B frame with the values it asserts, and fails on any other value."""
+    frame = oracle.load_dat(os.path.join(PKTS, "bench_frame.dat"))
+    assert oracle.packet_l4(frame, BENCH_WANT) == 0
+    for k in range(len(BENCH_WANT)):
+        w = list(BENCH_WANT)
+        w[k] ^= 1
+        assert oracle.packet_l4(frame, tuple(w)) != 0, k
+    assert oracle.packet_l4(frame[:40], BENCH_WANT) != 0          # Udp::parse fails
+
+
+def config1_want(hb):
+    """The values config 1's frames carry (rpkt_build.rs:13-27 headers), for packet_l4."""
+    r = oracle.parse_batch(hb.frames, hb.n, flags=3, stride=hb.stride)
+    keys = ("ip_src", "ip_dst", "ip_checksum", "ip_ident", "src_port", "dst_port", "l4_word6",
+            "l4_checksum")
+    assert all((r[k] == r[k][0]).all() for k in keys)            # 1000 identical frames
+    return tuple(int(r[k][0]) for k in keys)
+
+
+def test_packet_l4_loop_over_config1():
+    from rpkt_amd import gen
+    hb = gen.make_batch(1)
+    want = config1_want(hb)
+    assert want[6] == 30 and want[4] == 60376
+    assert oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, hb.frame_len or hb.stride, 3,
+                                 want) == 0
+    bad = list(want)
+    bad[3] ^= 0x100
+    assert oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, hb.frame_len or hb.stride, 2,
+                                 tuple(bad)) == 2 * hb.n
