@@ -24,6 +24,7 @@ ap.add_argument("--configs", default="2,3")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--launches", type=int, default=20)
 ap.add_argument("--variants", default="0,1,2,3,10")
+ap.add_argument("--rotate", type=int, default=8, help="distinct batches rotated at config 2")
 args = ap.parse_args()
 
 L = engine.lib()
@@ -33,7 +34,7 @@ L.rpkt_gpu_debug_variant.restype = ctypes.c_int
 variants = [int(v) for v in args.variants.split(",")]
 res = {}
 for cfg in [int(c) for c in args.configs.split(",")]:
-    R = 4 if cfg == 2 else 1
+    R = args.rotate if cfg == 2 else 1
     hbs = [gen.make_batch(cfg, seed=50 + r) for r in range(R)]
     dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
     recs = [engine.alloc_records(hb.n) for hb in hbs]
