@@ -42,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from rpkt_amd import dist as rdist, engine, fields, gen  # noqa: E402
-from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, F_FLOW_EV, as_records  # noqa: E402
+from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, as_records  # noqa: E402,E501
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -138,11 +138,11 @@ def launch_ranks(n, argv):
     return rc
 
 
-def algorithmic_bytes(hb, flow=False):
-    """Bytes one step must move: every frame byte read + the 80-B record written
-    (+ 4 B offset per frame for the packed layout; + 8 B flow event written and read
-    back by the flow-counter pass).  SURVEY.md §8d."""
-    b = int(hb.lens().sum()) + hb.n * REC_BYTES
+def algorithmic_bytes(hb, flow=False, rec_bytes=REC_BYTES):
+    """Bytes one step must move: every frame byte read + the record written (80 B, or
+    16 B compact) (+ 4 B offset per frame for the packed layout; + 8 B flow event
+    written and read back by the flow-counter pass).  SURVEY.md §8d."""
+    b = int(hb.lens().sum()) + hb.n * rec_bytes
     if isinstance(hb, gen.HostChains):             # segment descriptors + chain index
         return b + 8 * hb.n_segs + 4 * (hb.n + 1)
     if hb.offsets is not None:
@@ -152,7 +152,8 @@ def algorithmic_bytes(hb, flow=False):
     return b
 
 
-def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3):
+def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3,
+               compact=False):
     """Time `steps` launches (rotating over dbs).  Returns wall seconds (max over
     ranks) and the mean per-launch device time from two HIP events recorded on the
     launch stream around the back-to-back launches."""
@@ -169,6 +170,8 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
                               workspace=flow["ws"], stream=stream)
         elif isinstance(db, engine.DeviceChains):
             engine.parse_chains(db, flags, recs=rc, stream=stream)
+        elif compact:
+            engine.parse_batch_compact(db, flags, recs=rc, stream=stream)
         else:
             engine.parse_batch(db, flags, recs=rc, stream=stream)
 
@@ -374,7 +377,9 @@ def layout_name(hb):
     return ("stride%d" % hb.stride) if hb.stride else "packed+u32 offsets"
 
 
-def run_config(cfg, args, rank, world, cpu=False):
+def run_config(cfg, args, rank, world, cpu=False, compact=False):
+    """One parse leg: config `cfg`'s batches resident, K timed launches.  compact: the
+    16-byte record entry point (rpkt_gpu_parse_batch_compact) instead of the 80-byte one."""
     flags = gen.FLAGS[cfg]
     flow = None
     if cfg == 4:                                   # strong scaling: shard one 8M batch
@@ -394,7 +399,8 @@ def run_config(cfg, args, rank, world, cpu=False):
         scaling = "weak"
     dbs = [engine.DeviceChains.from_host(hb) if cfg in gen.CHAINED else
            engine.DeviceBatch.from_host(hb) for hb in hbs]
-    recs = [engine.alloc_records(hb.n) for hb in hbs]
+    rec_bytes = REC16_BYTES if compact else REC_BYTES
+    recs = [torch.empty(hb.n * rec_bytes, dtype=torch.uint8, device="cuda") for hb in hbs]
     if cfg == 4:
         nb = 8192
         flow = {"n_buckets": nb,
@@ -405,15 +411,15 @@ def run_config(cfg, args, rank, world, cpu=False):
     log(rank, "config %d: %d frames/rank x %d batches resident, flags=%d" % (
         cfg, hbs[0].n, len(hbs), flags))
     wall, kern_ms, warm = time_parse(dbs, recs, flags, args.steps, args.warmup, world, flow,
-                                     args.min_warmup_s)
+                                     args.min_warmup_s, compact)
 
     frames_step = sum(hb.n for hb in hbs) / len(hbs)
     bytes_step = sum(int(hb.lens().sum()) for hb in hbs) / len(hbs)
-    alg_step = sum(algorithmic_bytes(hb, flow is not None) for hb in hbs) / len(hbs)
+    alg_step = sum(algorithmic_bytes(hb, flow is not None, rec_bytes) for hb in hbs) / len(hbs)
     mpps = frames_step * world * args.steps / wall / 1e6
     gbps = bytes_step * world * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic(cfg)
+    traffic, tsrc = pmc_traffic(cfg) if not compact else pmc_traffic_tx("compact%d" % cfg)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
         "warmup_launches": warm,
@@ -423,7 +429,11 @@ def run_config(cfg, args, rank, world, cpu=False):
                      "traffic": traffic, "traffic_source": tsrc,
                      "alg_bytes_per_launch": int(alg_step)},
         "flags": FLAG_NAMES[flags], "layout": layout_name(hbs[0]),
+        "record_bytes": rec_bytes,
     }
+    if compact:
+        out["what"] = ("rpkt_gpu_parse_batch_compact: the same parse + sums, 16-B records "
+                       "(status, offsets, sums, verdicts)")
     if cfg == 4:
         torch.cuda.synchronize()
         barrier(world)
@@ -441,7 +451,7 @@ def run_config(cfg, args, rank, world, cpu=False):
         out["flow_pkts_total"] = int(c[:, 0].sum())
         # every launch (warmup included) added its shard's frames to the counters
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
-    if cpu and rank == 0:
+    if cpu and rank == 0 and not compact:
         g = as_records(recs[0].cpu().numpy())
         if cfg in gen.CHAINED:
             out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds,
@@ -597,6 +607,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
+    ap.add_argument("--compact", default="2,3",
+                    help="configs also timed with 16-B compact records (extra.config<N>_compact)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -644,6 +656,8 @@ def main():
     for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
         mode = next(m for m in ("build", "forward", "opts", "layers", "fields") if leg.startswith(m))
         extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
+    for c in [int(x) for x in args.compact.split(",") if x.strip()]:
+        extra["config%d_compact" % c] = run_config(c, args, rank, world, compact=True)
     if want_cpu and not args.no_config1:
         extra["config1"] = run_config1(args)
 

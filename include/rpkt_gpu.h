@@ -186,6 +186,34 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* batch, uint32_t flags,
                          rpkt_rec_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
                          uint32_t n_buckets, void* stream);
 
+/* Compact record: 16 bytes, the projection of rpkt_rec_t a caller needs to locate the
+ * layers and read the verdicts, for receive loops that read getters from the frame
+ * itself (rpkt's views hold only the buffer and read fields lazily,
+ * ipv4/generated.rs:17-20).  Fields equal the rpkt_rec_t fields of the same name;
+ * verdict bit 0 = RPKT_F_IP_SUM requested and ip_sum == 0xffff, bit 1 =
+ * RPKT_F_L4_SUM requested, status OK and (l4_sum == 0xffff or a UDP checksum field
+ * of 0: "not computed"). */
+typedef struct rpkt_rec16 {
+    uint8_t  status;            /*  0 enum rpkt_status                          */
+    uint8_t  n_vlan;            /*  1                                           */
+    uint8_t  ip_protocol;       /*  2                                           */
+    uint8_t  verdict;           /*  3 bit 0 IPv4 header sum ok, bit 1 L4 sum ok */
+    uint16_t l3_off;            /*  4                                           */
+    uint16_t l4_off;            /*  6                                           */
+    uint16_t payload_off;       /*  8                                           */
+    uint16_t payload_len;       /* 10                                           */
+    uint16_t ip_sum;            /* 12                                           */
+    uint16_t l4_sum;            /* 14                                           */
+} rpkt_rec16_t;
+
+#define RPKT_REC16_BYTES 16u
+
+/* rpkt_gpu_parse_batch writing rpkt_rec16_t records (recs_dev n * 16 B, 16-byte
+ * aligned): the same parse, sums and flow events, one fifth of the record bytes. */
+int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* batch, uint32_t flags,
+                                 rpkt_rec16_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
+                                 uint32_t n_buckets, void* stream);
+
 /* Accumulate flow events into counters_dev (u64[(n_buckets+1)*4], caller
  * zeroes it once; calls add).  workspace_dev must hold
  * rpkt_gpu_flow_workspace_bytes(n, n_buckets) bytes.  Calls that add into the

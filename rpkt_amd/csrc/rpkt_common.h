@@ -679,6 +679,19 @@ __device__ __forceinline__ uint64_t flow_event(const LaneRec& L, const uint32_t*
     return ev;
 }
 
+// The 16-byte compact record (rpkt_rec16_t) of a parsed frame, from the record words
+// (the projection of rpkt_rec_t documented in include/rpkt_gpu.h).
+__device__ __forceinline__ u32x4 compact_record(const LaneRec& L, uint32_t flags) {
+    const uint32_t* w = L.w;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;
+    uint32_t verdict = 0;
+    if ((flags & RPKT_F_IP_SUM) && (w[18] & 0xffffu) == 0xffffu) verdict |= 1u;
+    if ((flags & RPKT_F_L4_SUM) && L.status == RPKT_S_OK &&
+        ((w[18] >> 16) == 0xffffu || (proto == 17u && (w[15] & 0xffffu) == 0)))
+        verdict |= 2u;
+    return u32x4{(w[0] & 0xffffu) | (proto << 16) | (verdict << 24), w[16], w[17], w[18]};
+}
+
 // Records of the tile are staged through LDS (the window area, free once the parse
 // is done; stride 21 dwords: conflict-free) and stored as wave-instructions of 1 KiB
 // contiguous each, with non-temporal stores (measured -12 % at 64 B, -2 % at 1500 B

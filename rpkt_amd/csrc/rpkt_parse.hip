@@ -16,7 +16,9 @@ namespace {
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
 // 22 = default-policy stream loads, 23 = edge lines streamed first after the parse,
 // 24 = never, 25 = after the parse on long tiles).
-template <bool L4, int V>
+// C16: write the 16-byte compact record (rpkt_rec16_t) instead of the 80-byte one:
+// kept in registers, one 16-B store per lane (1 KiB contiguous per wave), no LDS stage.
+template <bool L4, int V, bool C16 = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -60,7 +62,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     } else {
         parse_lane(W, lane, fr, valid, flags, L);
     }
-    if constexpr (V != 3) stage_record(W, lane, L.w);
+    if constexpr (V != 3 && !C16) stage_record(W, lane, L.w);
 
     // 3. L4 bytes beyond the window: flattened chunk stream over the tile.  The stream
     // is read once: non-temporal loads (measured -13 % at 1500 B); the header windows
@@ -88,7 +90,8 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         }
         if (L.want_l4) {
             const uint32_t seg = be_sum(L.l4_part + sp, L.l4_start_abs);
-            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
+            if constexpr (C16) L.w[18] |= fold16(L.pseudo + seg) << 16;
+            else rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + seg) << 16;
         }
     }
     if constexpr (V == 3) {
@@ -101,10 +104,16 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
 
     // 4. records (+ flow events)
     if ((flags & RPKT_F_FLOW_EV) && valid) {
-        const uint64_t ev = flow_event(L, rec_stage(W) + lane * 21, n_buckets);
+        const uint64_t ev = flow_event(L, C16 ? L.w : rec_stage(W) + lane * 21, n_buckets);
         __builtin_nontemporal_store(ev, &flow_ev[i]);
     }
-    flush_records<V != 8>(W, lane, recs, p0, n);
+    if constexpr (C16) {
+        if (valid)
+            __builtin_nontemporal_store(compact_record(L, flags),
+                                        reinterpret_cast<u32x4*>(recs) + i);
+    } else {
+        flush_records<V != 8>(W, lane, recs, p0, n);
+    }
 }
 
 // ---- mbuf chains: the same parse over rpkt-dpdk's Pbuf ----
@@ -796,6 +805,29 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+
+int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,
+                                 rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
 }
 
 int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from .build import GPU_LIB
-from .records import LAYERS_BYTES, OPTS_BYTES, REC_BYTES, F_FLOW_EV
+from .records import LAYERS_BYTES, OPTS_BYTES, REC_BYTES, REC16_BYTES, F_FLOW_EV
 
 RPKT_OK = 0
 ERRORS = {-1: "RPKT_E_INVAL", -2: "RPKT_E_HIP", -3: "RPKT_E_TOO_LARGE", -4: "RPKT_E_ALIGN",
@@ -50,7 +50,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_checksum_chains_workspace_bytes", "rpkt_gpu_checksum_chains",
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
            "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch",
-           "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version"]
+           "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
+           "rpkt_gpu_parse_batch_compact"]
 
 _lib = None
 
@@ -78,6 +79,8 @@ def lib():
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p]
         L.rpkt_gpu_parse_batch.restype = ctypes.c_int
+        L.rpkt_gpu_parse_batch_compact.argtypes = L.rpkt_gpu_parse_batch.argtypes
+        L.rpkt_gpu_parse_batch_compact.restype = ctypes.c_int
         L.rpkt_gpu_flow_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.rpkt_gpu_flow_workspace_bytes.restype = ctypes.c_size_t
         L.rpkt_gpu_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
@@ -199,6 +202,22 @@ def parse_batch(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=Non
                                     flow_ev.data_ptr() if flow_ev is not None else None,
                                     n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_batch")
+    return (recs, flow_ev) if flags & F_FLOW_EV else recs
+
+
+def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):
+    """rpkt_gpu_parse_batch_compact: the same parse writing 16-byte rpkt_rec16_t
+    records; returns the uint8 record tensor (n * 16 bytes)."""
+    torch = _torch()
+    if recs is None:
+        recs = torch.empty(batch.n * REC16_BYTES, dtype=torch.uint8, device=batch.frames.device)
+    if flags & F_FLOW_EV and flow_ev is None:
+        flow_ev = torch.empty(batch.n, dtype=torch.int64, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_parse_batch_compact(ctypes.byref(d), flags, recs.data_ptr(),
+                                            flow_ev.data_ptr() if flow_ev is not None else None,
+                                            n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_batch_compact")
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
 
 

@@ -18,6 +18,38 @@ REC_DTYPE = np.dtype([
 ])
 assert REC_DTYPE.itemsize == REC_BYTES
 
+REC16_BYTES = 16
+REC16_DTYPE = np.dtype([          # rpkt_rec16_t (include/rpkt_gpu.h), 16 B
+    ("status", "u1"), ("n_vlan", "u1"), ("ip_protocol", "u1"), ("verdict", "u1"),
+    ("l3_off", "<u2"), ("l4_off", "<u2"), ("payload_off", "<u2"), ("payload_len", "<u2"),
+    ("ip_sum", "<u2"), ("l4_sum", "<u2"),
+])
+assert REC16_DTYPE.itemsize == REC16_BYTES
+
+
+def project16(recs, flags):
+    """The compact records rpkt_gpu_parse_batch_compact writes, from full records
+    (the projection include/rpkt_gpu.h defines; used to check the GPU against the
+    oracle's full records)."""
+    out = np.zeros(recs.shape[0], dtype=REC16_DTYPE)
+    for k in ("status", "n_vlan", "ip_protocol", "l3_off", "l4_off", "payload_off",
+              "payload_len", "ip_sum", "l4_sum"):
+        out[k] = recs[k]
+    ip_ok = (recs["ip_sum"] == 0xffff) & bool(flags & 1)
+    l4_ok = bool(flags & 2) & (recs["status"] == 0) & (
+        (recs["l4_sum"] == 0xffff) | ((recs["ip_protocol"] == 17) & (recs["l4_checksum"] == 0)))
+    out["verdict"] = ip_ok.astype(np.uint8) | (l4_ok.astype(np.uint8) << 1)
+    return out
+
+
+def as_records16(raw):
+    """View a uint8 buffer of n*16 bytes as compact records."""
+    a = np.asarray(raw)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a.reshape(-1).view(REC16_DTYPE)
+
+
 # enum rpkt_status (include/rpkt_gpu.h)
 STATUS = {
     "OK": 0, "ETH_SHORT": 1, "VLAN_SHORT": 2, "NOT_IPV4": 3, "IP_SHORT": 4,

@@ -58,6 +58,28 @@ def test_record_layout_matches_header():
     assert records.REC_BYTES == 80
 
 
+def test_rec16_layout_matches_header():
+    src = open(HDR).read()
+    offs = struct_offsets(src, "rpkt_rec16")
+    assert offs == [records.REC16_DTYPE.fields[n][1] for n in records.REC16_DTYPE.names]
+    assert records.REC16_BYTES == 16
+
+
+def test_projection_of_oracle_records():
+    """project16 keeps the record fields and derives the verdict bits as documented."""
+    from oracle import oracle
+    from rpkt_amd import gen
+    import numpy as np
+    hb = gen.make_batch(6, 4000, seed=3)
+    for flags in (0, 1, 2, 3):
+        r = oracle.parse_batch(hb.frames, hb.n, flags=flags, offsets=hb.offsets, stride=hb.stride)
+        c = records.project16(r, flags)
+        assert np.array_equal(c["l4_off"], r["l4_off"]) and np.array_equal(c["status"], r["status"])
+        assert not (c["verdict"] & 1).any() if not flags & 1 else (c["verdict"] & 1).any()
+        assert not (c["verdict"] & 2).any() if not flags & 2 else (c["verdict"] & 2).any()
+        assert ((c["verdict"] & 2) == 0)[r["status"] != 0].all()
+
+
 def test_opts_layout_matches_header():
     src = open(HDR).read()
     offs = struct_offsets(src, "rpkt_opts")

@@ -296,3 +296,53 @@ def test_checksum_chains_match_from_buf(torch):
     for p in range(0, n_chains, 3):
         parts = [buf[s:s + l].tobytes() for s, l in segs[first[p]:first[p + 1]]]
         assert got[p] == oracle.from_buf(parts), p
+
+
+# ---- compact records (rpkt_gpu_parse_batch_compact) ---------------------------------
+
+def gpu_records16(hb, flags=3, n_buckets=0):
+    from rpkt_amd.records import as_records16
+    db = engine.DeviceBatch.from_host(hb)
+    if flags & F_FLOW_EV:
+        recs, ev = engine.parse_batch_compact(db, flags, n_buckets=n_buckets)
+        return as_records16(recs.cpu().numpy()), ev.cpu().numpy().view(np.uint64)
+    return as_records16(engine.parse_batch_compact(db, flags).cpu().numpy())
+
+
+def assert_same16(g, o):
+    if g.tobytes() == o.tobytes():
+        return
+    bad = np.nonzero(g != o)[0]
+    i = int(bad[0])
+    fields = [f for f in g.dtype.names if g[i][f] != o[i][f]]
+    raise AssertionError("%d compact records differ; first #%d fields %s gpu=%s oracle=%s" % (
+        bad.size, i, fields, [g[i][f] for f in fields], [o[i][f] for f in fields]))
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6])
+def test_compact_records_equal_projected_oracle(torch, cfg):
+    """The 16-byte records equal the oracle's full records projected (status, offsets,
+    sums, verdict bits), full BASELINE sizes for configs 2-5, the fuzz mix for 6."""
+    from rpkt_amd.records import project16
+    hb = gen.make_batch(cfg)
+    flags = gen.FLAGS.get(cfg, 3)
+    assert_same16(gpu_records16(hb, flags), project16(oracle_records(hb, flags), flags))
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_compact_flag_combinations_and_flow_events(torch, flags):
+    from rpkt_amd.records import project16
+    hb = gen.make_batch(6, 60000, seed=77)
+    nb = 4096
+    g, gev = gpu_records16(hb, flags | F_FLOW_EV, nb)
+    o, oev = oracle_records(hb, flags, nb, flow=True)
+    assert_same16(g, project16(o, flags))
+    assert np.array_equal(gev, oev)
+
+
+@pytest.mark.parametrize("lead", [0, 1, 3, 7, 13])
+def test_compact_fixtures_alignment(torch, lead):
+    from rpkt_amd.records import project16
+    _, frames = fixtures()
+    hb = host_batch(frames, lead)
+    assert_same16(gpu_records16(hb), project16(oracle_records(hb), 3))
