@@ -346,3 +346,27 @@ def test_compact_fixtures_alignment(torch, lead):
     _, frames = fixtures()
     hb = host_batch(frames, lead)
     assert_same16(gpu_records16(hb), project16(oracle_records(hb), 3))
+
+
+# ---- strided batches of short frames at every stride phase -----------------------------
+
+@pytest.mark.parametrize("stride,flen", [(64, 64), (64, 60), (64, 14), (48, 48), (49, 49),
+                                         (40, 40), (80, 64), (32, 20), (64, 65), (96, 96)])
+def test_short_strided_frames(torch, stride, flen):
+    """Strided batches of short frames (strides that are and are not multiples of 16, so
+    every 16-B phase of a window occurs): fuzzed headers of every status cut to flen
+    bytes, records bit-exact vs the oracle, full and compact."""
+    from rpkt_amd.records import project16
+    src = gen.make_batch(6, 20000, seed=stride * 131 + flen)
+    n = src.n
+    buf = np.zeros(n * stride + 64, dtype=np.uint8)
+    lens = src.lens()
+    for i in range(n):
+        a = int(src.offsets[i])
+        k = min(int(lens[i]), flen)
+        buf[i * stride:i * stride + k] = src.frames[a:a + k]
+    hb = gen.HostBatch(6, n, 0, buf, None, stride, flen)
+    for flags in (1, 3):
+        o = oracle_records(hb, flags)
+        assert_same(gpu_records(hb, flags), o)
+        assert_same16(gpu_records16(hb, flags), project16(o, flags))
