@@ -55,6 +55,8 @@ constexpr int kStreamUnroll = 4;     // 16-B chunk loads in flight per lane per 
 constexpr int kChainStreamUnroll = 8;  // the same in the mbuf-chain kernel
 constexpr uint64_t kMaxFrameBytes = 0xffffff00ull;  // voffset + 16 never wraps
 constexpr uint32_t kSplitStreamBytes = 65536;  // tile stream above which edge lines go first
+constexpr uint32_t kEdgeWindowBytes = 32768;   // tile stream above which the window phase
+                                               // sums the edge lines (edge_lines_window)
 
 struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit a CU
     uint8_t  win[kWave * kSlot];     // header windows, slot stride 132 B
@@ -370,6 +372,74 @@ __device__ __forceinline__ uint32_t gbyte(__amdgpu_buffer_rsrc_t rs, uint32_t a)
 }
 
 struct Frame { uint32_t off, len; };
+
+// Edge lines in the window phase (every tile).  The same split as edge_lines_first --
+// a frame's partial head line [wend, he) and partial tail line [tb, fend) summed
+// early, the stream then covering only [he, tb) -- but the edge chunks are loaded
+// with the window, by the same cooperative mapping (chunk k of lane l: piece l % 8 of
+// frame 8k + l / 8), and each frame's eight chunk sums are added by three DPP steps
+// within its 8 lanes.  No scan, no extra pass: the head line is fetched once with
+// the window it shares a line with, the tail line together with the next frame's
+// window.  Sums land in W.first / W.last (free until the stream), one per frame.
+__device__ __forceinline__ uint32_t sum8_lanes(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0xb1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x4e, 0xf, 0xf, false);   // quad_perm 2,3,0,1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    return x;                                                          // lane 8m: the sum
+}
+
+__device__ __forceinline__ void edge_spans(uint32_t qo, uint32_t ql, uint32_t& wend,
+                                           uint32_t& fend, uint32_t& he, uint32_t& tb) {
+    wend = (qo & ~15u) + kWin;
+    fend = qo + ql;
+    const bool has = fend > wend;
+    he = has ? min((wend + 127u) & ~127u, fend) : 0u;
+    tb = has ? max(fend & ~127u, he) : 0u;
+}
+
+template <int AUX = 0>
+__device__ __forceinline__ EdgeLines edge_lines_window(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                       WaveScratch& W, int lane, Frame fr,
+                                                       bool valid, uint32_t min_tile_stream) {
+    {
+        const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
+        const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
+        if (wave_sum(span) <= min_tile_stream) return EdgeLines{false, 0u, 0u, 0u};  // uniform
+    }
+    const int j = lane & 7;
+    u32x4 d[kWinChunks];
+    uint32_t lim[kWinChunks], a0[kWinChunks];
+    // head chunks, then tail chunks: 8 loads in flight per pass
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) {
+            const int q = (k * kWave + lane) >> 3;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t ql = (uint32_t)__shfl((int)(valid ? fr.len : 0u), q, kWave);
+            uint32_t wend, fend, he, tb;
+            edge_spans(qo, ql, wend, fend, he, tb);
+            const uint32_t a = pass == 0 ? wend + 16u * j : tb + 16u * j;
+            const uint32_t e = pass == 0 ? he : fend;
+            const bool in = a < e && (pass == 0 || tb < fend);
+            a0[k] = a;
+            lim[k] = in ? (e - a < 16u ? e - a : 16u) : 0u;
+            d[k] = load16_fast<AUX>(rs, in ? a : fb);
+        }
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) {
+            u32x4 v = d[k];
+            if (__builtin_expect(lim[k] != 0 && straddles(a0[k], fb), 0)) v = load16(rs, a0[k], fb);
+            const uint32_t x = sum8_lanes(lim[k] ? chunk_sum(v, 0, (int)lim[k]) : 0u);
+            if (j == 0) (pass == 0 ? W.first : W.last)[(k * kWave + lane) >> 3] = x;
+        }
+    }
+    wave_sync();
+    uint32_t wend, fend, he, tb;
+    edge_spans(fr.off, valid ? fr.len : 0u, wend, fend, he, tb);
+    return EdgeLines{true, W.first[lane] + W.last[lane], he, tb};
+}
+
 
 __device__ __forceinline__ Frame frame_span(const uint32_t* offsets, uint32_t stride,
                                             uint32_t frame_len, uint32_t frames_bytes,

@@ -15,7 +15,9 @@ namespace {
 // tools/ablate.py (0 = the product kernel; 1 = no parse, 3 = no record stores,
 // 8 = plain instead of non-temporal record stores, 21 = nt window loads too,
 // 22 = default-policy stream loads, 23 = edge lines streamed first after the parse,
-// 24 = never, 25 = after the parse on long tiles).
+// 24 = never, 25 = after the parse on long tiles, 40 / 41 / 43 = edge lines with the
+// window on tiles streaming more than 0 / 16 / 64 KB (the product: 32 KB), 44 = the
+// round-1 edge_lines_first pass on tiles streaming more than 64 KB).
 // C16: write the 16-byte compact record (rpkt_rec16_t) instead of the 80-byte one:
 // kept in registers, one 16-B store per lane (1 KiB contiguous per wave), no LDS stage.
 template <bool L4, int V, bool C16 = false>
@@ -45,7 +47,13 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
         window_commit(W, rs, frames_bytes, d, addr, fix, lane);
     }
     EdgeLines X{false, 0u, 0u, 0u};
-    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25)
+    // tiles streaming more than 32 KB sum their frames' edge lines with the window
+    // (edge_lines_window; profiles/r02_edge_window: config 5 -1.2 % time and -9 % read
+    // traffic, configs 3 and 4 unchanged in time; every tile: config 4 +10 %)
+    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
+        X = edge_lines_window(rs, frames_bytes, W, lane, fr, valid,
+                              V == 40 ? 0u : V == 41 ? 16384u : V == 43 ? 65536u : kEdgeWindowBytes);
+    else if constexpr (L4 && V == 44)                  // the round-1 split: a pass after the window
         X = edge_lines_first(rs, frames_bytes, W, lane, valid, wend, fend);
     wave_sync();
 
@@ -873,6 +881,11 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 23: return RPKT_V(23);
         case 24: return RPKT_V(24);
         case 25: return RPKT_V(25);
+        case 40: return RPKT_V(40);
+        case 41: return RPKT_V(41);
+        case 42: return RPKT_V(42);
+        case 43: return RPKT_V(43);
+        case 44: return RPKT_V(44);
         case 10:
             return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),

@@ -20,8 +20,9 @@ from rpkt_amd import engine, gen  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--launches", type=int, default=20)
-ap.add_argument("--frames", default="1,2,4,8")
+ap.add_argument("--frames", default="4,404,804,402,802,408,808", help="F + 100 P")
 ap.add_argument("--n", type=int, default=0)
+ap.add_argument("--config", type=int, default=9, help="9 = the capture mix, else a bench config")
 args = ap.parse_args()
 
 L = engine.lib()
@@ -29,7 +30,8 @@ L.rpkt_gpu_debug_layers_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes
                                             ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_layers_variant.restype = ctypes.c_int
 variants = [int(v) for v in args.frames.split(",")]
-hb = gen.make_mix(args.n or gen.DEFAULT_N[9], seed=gen.DEFAULT_SEED[9])
+hb = (gen.make_mix(args.n or gen.DEFAULT_N[9], seed=gen.DEFAULT_SEED[9]) if args.config == 9
+      else gen.make_batch(args.config, args.n or None))
 db = engine.DeviceBatch.from_host(hb)
 desc = db.desc()
 outs = {v: torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda") for v in variants}
@@ -52,4 +54,4 @@ ref = outs[variants[0]].cpu().numpy()
 same = {"F%d" % v: bool(np.array_equal(outs[v].cpu().numpy(), ref)) for v in variants}
 out = {"F%d" % v: {"us": round(float(np.median(times[v])), 2), "min_us": round(min(times[v]), 2)}
        for v in variants}
-print(json.dumps({"n": hb.n, "times": out, "identical": same}))
+print(json.dumps({"config": args.config, "n": hb.n, "times": out, "identical": same}))
