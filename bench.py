@@ -204,19 +204,34 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
     return wall, kern_ms, warm_launches
 
 
-def pmc_traffic(cfg):
-    """Per-launch HBM traffic of parse_kernel for this config from the rocprofv3 PMC
-    summary committed under profiles/ (tools/traffic.py), when it was measured on
-    this exact engine build; else None."""
-    path = os.path.join(ROOT, "profiles", "traffic_c%d.json" % cfg)
+def pmc_traffic(cfg, compact=False):
+    """Per-launch HBM traffic of parse_kernel for this config (and record size) from the
+    rocprofv3 PMC summary committed under profiles/ (tools/traffic.py), when it was
+    measured on this exact engine build; else None."""
+    path = os.path.join(ROOT, "profiles", "traffic_c%d%s.json" % (cfg, "_compact" if compact else ""))
     try:
         with open(path) as fh:
             t = json.load(fh)
     except (OSError, ValueError):
         return None, None
-    if t.get("engine_build") != engine.lib().rpkt_gpu_build_info().decode():
+    if not same_unit(t.get("engine_build"), "parse"):
         return None, None
     return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
+def same_unit(profiled_build, unit):
+    """Whether a profile taken on engine build `profiled_build` measured the same source
+    of kernel unit `unit` (rpkt_<unit>.hip + the shared headers) as the loaded build."""
+    def unit_hash(b):
+        for tok in (b or "").replace(";", " ").split():
+            if tok.startswith(unit + "="):
+                return tok
+        return None
+    cur = engine.lib().rpkt_gpu_build_info().decode()
+    if profiled_build == cur:
+        return True
+    h = unit_hash(cur)
+    return h is not None and h == unit_hash(profiled_build)
 
 
 def pmc_traffic_tx(leg):
@@ -228,7 +243,9 @@ def pmc_traffic_tx(leg):
             t = json.load(fh)
     except (OSError, ValueError):
         return None, None
-    if t.get("engine_build") != engine.lib().rpkt_gpu_build_info().decode() or leg not in t["legs"]:
+    unit = {"build": "tx", "forward": "tx", "opts": "walks", "layers": "walks",
+            "fields": "fields"}[leg.rstrip("0123456789")]
+    if leg not in t["legs"] or not same_unit(t.get("engine_build"), unit):
         return None, None
     return int(t["legs"][leg]["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
 
@@ -419,7 +436,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
     mpps = frames_step * world * args.steps / wall / 1e6
     gbps = bytes_step * world * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic(cfg) if not compact else pmc_traffic_tx("compact%d" % cfg)
+    traffic, tsrc = pmc_traffic(cfg, compact)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
         "warmup_launches": warm,
@@ -607,6 +624,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
+    ap.add_argument("--record", default="full", choices=["full", "compact"],
+                    help="record size of the main leg (profiling the compact kernel alone)")
     ap.add_argument("--compact", default="2,3",
                     help="configs also timed with 16-B compact records (extra.config<N>_compact)")
     args = ap.parse_args()
@@ -648,7 +667,8 @@ def main():
     if not args.cpu_threads:
         args.cpu_threads = usable_cpus()
 
-    main_res = run_config(args.config, args, rank, world, cpu=want_cpu)
+    main_res = run_config(args.config, args, rank, world, cpu=want_cpu,
+                          compact=args.record == "compact")
     extra = {}
     for c in [int(x) for x in args.also.split(",") if x.strip()]:
         if c != args.config:

@@ -35,14 +35,23 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def source_hash():
-    """Short hash of the engine sources: ties profiles/ numbers to a kernel build."""
+def source_hash(units=None):
+    """Short hash of the engine sources (or of some units plus the shared headers):
+    ties profiles/ numbers to a kernel build."""
     import hashlib
     h = hashlib.sha1()
-    for f in GPU_SRC + GPU_DEPS + HDR:
+    srcs = GPU_SRC if units is None else [f for f in GPU_SRC if os.path.basename(f) in units]
+    for f in srcs + GPU_DEPS + HDR:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]
+
+
+def unit_hashes():
+    """Per-unit hashes (unit file + shared headers), so a profile of one kernel family
+    stays valid while another unit changes: "parse=... tx=... walks=... fields=..."."""
+    return " ".join("%s=%s" % (u, source_hash(["rpkt_%s.hip" % u]))
+                    for u in ("parse", "tx", "walks", "fields"))
 
 
 def build_gpu(force=False, extra=()):
@@ -52,7 +61,8 @@ def build_gpu(force=False, extra=()):
     if not (force or _stale(GPU_LIB, GPU_SRC + GPU_DEPS + HDR)):
         return GPU_LIB
     flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-             '-DRPKT_SRC_HASH="%s"' % source_hash()] + list(extra)
+             '-DRPKT_SRC_HASH="%s"' % source_hash(), '-DRPKT_UNIT_HASHES="%s"' % unit_hashes()] + \
+        list(extra)
     objs = [os.path.join(OUT, os.path.basename(f).replace(".hip", ".o")) for f in GPU_SRC]
     with ThreadPoolExecutor(max_workers=len(GPU_SRC)) as ex:
         list(ex.map(lambda so: subprocess.check_call(flags + ["-c", "-o", so[1], so[0]]),

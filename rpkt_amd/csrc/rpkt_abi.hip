@@ -15,8 +15,12 @@ uint32_t rpkt_gpu_abi_version(void) { return RPKT_ABI_VERSION; }
 #ifndef RPKT_SRC_HASH
 #define RPKT_SRC_HASH "dev"
 #endif
+#ifndef RPKT_UNIT_HASHES
+#define RPKT_UNIT_HASHES "dev"
+#endif
 const char* rpkt_gpu_build_info(void) {
-    return "rpkt_gpu src=" RPKT_SRC_HASH " gfx950; rec=80B; tile=64 frames/wave; win=128B";
+    return "rpkt_gpu src=" RPKT_SRC_HASH " gfx950; rec=80B; tile=64 frames/wave; win=128B; "
+           RPKT_UNIT_HASHES;
 }
 
 const char* rpkt_gpu_status_name(int s) {

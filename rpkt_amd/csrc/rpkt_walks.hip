@@ -726,7 +726,9 @@ __device__ __forceinline__ int lay_next(const LayHdr& H, const LayTable& T, uint
 // most steps of the wave, most steps waited a full memory latency for one lane's
 // refill.  Chunks wholly past the frame end are not loaded (read as zeros).
 constexpr int kLayFrames = 4;
-constexpr int kLayPrefetch = 8;
+// measured slower (profiles/r02_layers: 84 -> 90 us at P = 4 or 8, F = 4): the walk is
+// VALU-bound, not waiting on the refills, and the prefetch adds registers and VALU
+constexpr int kLayPrefetch = 0;
 
 template <int P>
 struct NextWin {

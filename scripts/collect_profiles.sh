@@ -5,8 +5,9 @@
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
-for t in ${TAGS:-c2 c3 c4 c5 c7 walks build3}; do
-    P=$G/prof_$t; D=$R/profiles/r01_$t
+RND=${RND:-r02}
+for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact walks build3}; do
+    P=$G/prof_$t; D=$R/profiles/${RND}_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
     for k in fetch write; do
@@ -17,6 +18,8 @@ for t in ${TAGS:-c2 c3 c4 c5 c7 walks build3}; do
         python3 "$R/tools/traffic.py" "$P" tx:build3 "$R/profiles/traffic_tx.json"
     elif [ "$t" = walks ]; then
         python3 "$R/tools/traffic.py" "$P" tx "$R/profiles/traffic_tx.json"
+    elif [ "${t%_compact}" != "$t" ]; then
+        c=${t#c}; python3 "$R/tools/traffic.py" "$P" "${c%_compact}" "$R/profiles/traffic_$t.json"
     else
         python3 "$R/tools/traffic.py" "$P" "${t#c}" "$R/profiles/traffic_$t.json"
     fi

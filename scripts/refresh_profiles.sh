@@ -7,5 +7,8 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 for c in 2 3 4 5 7; do
     bash "$R/scripts/profile.sh" "c$c" "$c"
 done
+for c in 2 3; do
+    bash "$R/scripts/profile.sh" "c${c}_compact" "$c" --record compact
+done
 bash "$R/scripts/profile.sh" walks 2 --tx layers9,opts5,forward2,build2,fields9
 bash "$R/scripts/profile.sh" build3 2 --tx build3
