@@ -41,7 +41,11 @@ def source_hash(units=None):
     import hashlib
     h = hashlib.sha1()
     srcs = GPU_SRC if units is None else [f for f in GPU_SRC if os.path.basename(f) in units]
-    for f in srcs + GPU_DEPS + HDR:
+    deps = GPU_DEPS
+    if units is not None:                  # the generated table is the walk unit's alone
+        deps = [d for d in GPU_DEPS if not d.endswith("rpkt_proto_table.h") or
+                "rpkt_walks.hip" in units]
+    for f in srcs + deps + HDR:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]

@@ -720,51 +720,9 @@ __device__ __forceinline__ int lay_next(const LayHdr& H, const LayTable& T, uint
 // that walks several frames in a row evens the depths out over the wave.  The first
 // frame's window is staged cooperatively (coalesced 16-B loads).  Records are stored
 // per lane (64 B each).
-// P > 0: a lane's next frame's first P 16-B chunks are loaded into registers as soon
-// as it starts a frame, and moved into its slot when the frame ends: without it (P = 0)
-// the slot is refilled from memory at that point, and since some lane ends a frame in
-// most steps of the wave, most steps waited a full memory latency for one lane's
-// refill.  Chunks wholly past the frame end are not loaded (read as zeros).
 constexpr int kLayFrames = 4;
-// measured slower (profiles/r02_layers: 84 -> 90 us at P = 4 or 8, F = 4): the walk is
-// VALU-bound, not waiting on the refills, and the prefetch adds registers and VALU
-constexpr int kLayPrefetch = 0;
 
-template <int P>
-struct NextWin {
-    u32x4 d[P > 0 ? P : 1];
-    uint32_t fix;                                            // chunks straddling the buffer end
-    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t fb, Frame f) {
-        const uint32_t a = f.off & ~15u, e = f.off + f.len;
-        fix = 0;
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            const uint32_t c = a + 16u * k;
-            const bool in = c < e;
-            d[k] = load16_fast(rs, in ? c : fb);
-            fix |= (uint32_t)(in && straddles(c, fb)) << k;
-        }
-    }
-    // into the lane's slot; the window then covers frame bytes [0, 16 P - phase)
-    __device__ __forceinline__ void commit(LayerWin& Wn, Frame f) {
-        uint32_t* w = reinterpret_cast<uint32_t*>(Wn.base);
-        const uint32_t a = f.off & ~15u;
-#pragma unroll
-        for (int k = 0; k < P; ++k) {
-            u32x4 v = d[k];
-            if (__builtin_expect(fix & (1u << k), 0)) v = lay_edge16(Wn.rs, a + 16u * k, Wn.fb);
-            w[4 * k] = v.x;
-            w[4 * k + 1] = v.y;
-            w[4 * k + 2] = v.z;
-            w[4 * k + 3] = v.w;
-        }
-        Wn.off = f.off;
-        Wn.bias = f.off & 15u;
-        Wn.avail = 16u * P - (f.off & 15u);
-    }
-};
-
-template <int F, int P>
+template <int F>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -819,9 +777,6 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 
     LayerWin Wn{&W.win[lane * kLaySlot], fr[0].off & 15u, (uint32_t)(kLayChunks * 16) - (fr[0].off & 15u),
                 fr[0].off, fb, rs};
-    NextWin<P> nxt;
-    if constexpr (P > 0 && F > 1)
-        if (p0 + lane + kWave < n) nxt.issue(rs, fb, fr[1]);
     uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0;
@@ -887,29 +842,20 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 s = 0, e = f.len, nl = 0, g = RPKT_G_ETHER;
                 Wn.off = f.off;
                 if (active) {
-                    if constexpr (P > 0) {
-                        nxt.commit(Wn, f);
-                        Frame f2 = fr[0];                  // the frame after this one
-#pragma unroll
-                        for (int k = 1; k < F; ++k) f2 = fk + 1 == (uint32_t)k ? fr[k] : f2;
-                        if (fk + 1 < (uint32_t)F && i + kWave < n) nxt.issue(rs, fb, f2);
-                        H = lay_hdr(Wn, 0u, true);
-                    } else {
-                        Wn.refill(0u);
-                        H = lay_hdr(Wn, 0u, false);
-                    }
+                    Wn.refill(0u);
+                    H = lay_hdr(Wn, 0u, false);
                 }
             }
         }
     }
 }
 
-template <int F, int P>
+template <int F>
 int launch_layers(const rpkt_batch_t* b, uint32_t flen, rpkt_layers_t* layers_dev, void* stream) {
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t waves = (uint32_t)((b->n + (uint64_t)kWave * F - 1) / ((uint64_t)kWave * F));
     const uint32_t grid = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    return launch(layers_kernel<F, P>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    return launch(layers_kernel<F>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
                   layers_dev);
 }
@@ -942,12 +888,14 @@ int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
     if (((uintptr_t)layers_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    return launch_layers<kLayFrames, kLayPrefetch>(b, flen, layers_dev, stream);
+    return launch_layers<kLayFrames>(b, flen, layers_dev, stream);
 }
 
 // Development hook (not part of include/rpkt_gpu.h): the walk with F frames per lane
-// (1, 2, 4, 8) and P prefetched chunks of the next frame (variant = F + 100 P, P in
-// 0, 4, 8), for timing the choice of kLayFrames and kLayPrefetch.
+// (1, 2, 4, 8), for timing the choice of kLayFrames.  (Tried and dropped, DESIGN.md:
+// prefetching a lane's next frame window into registers, 84 -> 90 us; per-group steps
+// specialised at compile time and run one uniform group after another, 84 -> 195 us
+// on the capture mix, whose waves hold many groups per step.)
 int rpkt_gpu_debug_layers_variant(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, int frames,
                                   void* stream) {
     if (!b || !layers_dev || b->n == 0 || !b->frames_dev) return RPKT_E_INVAL;
@@ -955,16 +903,10 @@ int rpkt_gpu_debug_layers_variant(const rpkt_batch_t* b, rpkt_layers_t* layers_d
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     switch (frames) {
-        case 1: return launch_layers<1, 0>(b, flen, layers_dev, stream);
-        case 2: return launch_layers<2, 0>(b, flen, layers_dev, stream);
-        case 4: return launch_layers<4, 0>(b, flen, layers_dev, stream);
-        case 8: return launch_layers<8, 0>(b, flen, layers_dev, stream);
-        case 402: return launch_layers<2, 4>(b, flen, layers_dev, stream);
-        case 404: return launch_layers<4, 4>(b, flen, layers_dev, stream);
-        case 408: return launch_layers<8, 4>(b, flen, layers_dev, stream);
-        case 802: return launch_layers<2, 8>(b, flen, layers_dev, stream);
-        case 804: return launch_layers<4, 8>(b, flen, layers_dev, stream);
-        case 808: return launch_layers<8, 8>(b, flen, layers_dev, stream);
+        case 1: return launch_layers<1>(b, flen, layers_dev, stream);
+        case 2: return launch_layers<2>(b, flen, layers_dev, stream);
+        case 4: return launch_layers<4>(b, flen, layers_dev, stream);
+        case 8: return launch_layers<8>(b, flen, layers_dev, stream);
         default: return RPKT_E_INVAL;
     }
 }

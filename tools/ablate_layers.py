@@ -20,7 +20,7 @@ from rpkt_amd import engine, gen  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--launches", type=int, default=20)
-ap.add_argument("--frames", default="4,404,804,402,802,408,808", help="F + 100 P")
+ap.add_argument("--frames", default="1,2,4,8")
 ap.add_argument("--n", type=int, default=0)
 ap.add_argument("--config", type=int, default=9, help="9 = the capture mix, else a bench config")
 args = ap.parse_args()
