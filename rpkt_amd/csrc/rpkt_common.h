@@ -262,6 +262,7 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
                                                     uint32_t s_abs, uint32_t e_abs,
                                                     WaveScratch& W, int lane) {
     const bool ne = e_abs > s_abs;
+    if (__ballot(ne) == 0) return 0u;          // uniform: no range in the wave, no loads
     const uint32_t S = (s_abs + 15u) & ~15u, E = e_abs & ~15u;
     // edge chunks: head [s, min(e, S)) in the chunk at floor16(s); tail [max(s, E), e)
     // in the chunk at E when that is not the head chunk

@@ -301,6 +301,14 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
     const Frame fr = spans.get(i);
+    // the forbidden-source list (up to 128 addresses, searched in LDS) is loaded with
+    // the window, not after the parse: one memory round trip per wave instead of two
+    const bool list_in_lds = fwd.n_forbid != 0 && fwd.n_forbid <= 2u * kWave;
+    uint32_t fl0 = 0, fl1 = 0;
+    if (list_in_lds) {
+        if ((uint32_t)lane < fwd.n_forbid) fl0 = fwd.forbid_dev[lane];
+        if ((uint32_t)lane + kWave < fwd.n_forbid) fl1 = fwd.forbid_dev[lane + kWave];
+    }
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
@@ -356,12 +364,11 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     if (fwd.n_forbid) {                                         // :111-118, sorted list
         // up to 128 addresses are searched in LDS (W.s and W.e, contiguous, free once
         // the stream is done), a longer list in global memory
-        const bool in_lds = fwd.n_forbid <= 2u * kWave;
         const uint32_t* list = fwd.forbid_dev;
-        if (in_lds) {
+        if (list_in_lds) {
             uint32_t* t = W.s;
-            if ((uint32_t)lane < fwd.n_forbid) t[lane] = fwd.forbid_dev[lane];
-            if ((uint32_t)lane + kWave < fwd.n_forbid) t[lane + kWave] = fwd.forbid_dev[lane + kWave];
+            t[lane] = fl0;
+            t[lane + kWave] = fl1;
             wave_sync();
             list = t;
         }

@@ -28,7 +28,7 @@ L.rpkt_gpu_debug_forward_variant.argtypes = [ctypes.POINTER(engine.Batch), ctype
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_forward_variant.restype = ctypes.c_int
 variants = [int(v) for v in args.variants.split(",")]
-R = 4
+R = 8                                  # cache-free rotation (like bench.py config 2)
 hbs = [gen.make_batch(2, seed=60 + r) for r in range(R)]
 dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
 descs = [db.desc() for db in dbs]
