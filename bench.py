@@ -502,14 +502,14 @@ FIELD_LEG = [("ETHER_ETHERFRAME", "dst_addr"), ("ETHER_ETHERFRAME", "src_addr"),
 def run_tx(cfg, mode, args, rank, world):
     """TX side: rpkt_gpu_build_batch (headers + both checksums filled, the
     rpkt_build.rs path) or rpkt_gpu_forward_batch (loopback_rx rewrite) over a
-    resident batch whose records come from rpkt_gpu_parse_batch.  Rotates over 4
+    resident batch whose records come from rpkt_gpu_parse_batch.  Rotates over 8
     batches at 64 B like config 2.  Algorithmic bytes per frame: build = 80 B record
     read + the frame read once (checksums) + the fixed header bytes written;
     forward (fused parse + verdict + rewrite) = the frame read once + the 42 rewritten
     header bytes of forwarded frames + 1 B verdict."""
     torch.cuda.empty_cache()
     n = args.frames or gen.DEFAULT_N[cfg]
-    R = 4 if cfg == 2 else 1
+    R = 8 if cfg == 2 else 1                  # 64-B legs: 512 MiB of frames, past the cache
     if cfg == 9:                                   # protocol mix (captures + fuzz)
         hbs = [gen.make_mix(n, seed=gen.DEFAULT_SEED[9] + 7919 * rank)]
     else:

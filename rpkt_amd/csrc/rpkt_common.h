@@ -578,7 +578,14 @@ __device__ __forceinline__ uint32_t raw_range_sum(const uint8_t* slot, const uin
     uint32_t acc = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) acc = hsum(a0 + 4 * k < e ? R[k] : 0u, acc);
-    for (uint32_t a = a0 + 4 * N; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    // four reads in flight per round trip (a long in-window L4 span is up to ~24 dwords)
+    uint32_t a = a0 + 4 * N;
+    for (; a + 12u < e; a += 16u) {
+        const uint32_t x0 = lds32(slot, a), x1 = lds32(slot, a + 4u);
+        const uint32_t x2 = lds32(slot, a + 8u), x3 = lds32(slot, a + 12u);
+        acc = hsum(x3, hsum(x2, hsum(x1, hsum(x0, acc))));
+    }
+    for (; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
     acc -= halves(low_bytes(R[0], s & 3u));
     if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
     return acc;

@@ -75,7 +75,13 @@ __device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20]
 __device__ __forceinline__ uint32_t lds_range_sum(const uint8_t* slot, uint32_t s, uint32_t e) {
     if (e <= s) return 0u;
     uint32_t acc = 0;
-    for (uint32_t a = s & ~3u; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    uint32_t a = s & ~3u;
+    for (; a + 12u < e; a += 16u) {                  // four reads in flight per round trip
+        const uint32_t x0 = lds32(slot, a), x1 = lds32(slot, a + 4u);
+        const uint32_t x2 = lds32(slot, a + 8u), x3 = lds32(slot, a + 12u);
+        acc = hsum(x3, hsum(x2, hsum(x1, hsum(x0, acc))));
+    }
+    for (; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
     acc -= halves(low_bytes(lds32(slot, s & ~3u), s & 3u));
     if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
     return acc;
