@@ -17,7 +17,8 @@ namespace {
 // 22 = default-policy stream loads, 23 = edge lines streamed first after the parse,
 // 24 = never, 25 = after the parse on long tiles, 40 / 41 / 43 = edge lines with the
 // window on tiles streaming more than 0 / 16 / 64 KB (the product: 32 KB), 44 = the
-// round-1 edge_lines_first pass on tiles streaming more than 64 KB).
+// round-1 edge_lines_first pass on tiles streaming more than 64 KB, 45 = default-policy
+// window loads without the L4 stream).
 // C16: write the 16-byte compact record (rpkt_rec16_t) instead of the 80-byte one:
 // kept in registers, one 16-B store per lane (1 KiB contiguous per wave), no LDS stage.
 template <bool L4, int V, bool C16 = false>
@@ -43,7 +44,12 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
-        const uint32_t fix = window_issue<(V == 21) ? 2 : 0>(rs, frames_bytes, fr, lane, d, addr);
+        // header-only batches read each frame line once: non-temporal window loads
+        // (config 2: 27.2 -> 26.1 us, profiles/r02_ablate_c2_v21.log); with the L4
+        // stream the window's lines are shared with the stream, and nt there costs
+        // +13-30 % (configs 3-5)
+        constexpr int kWinAux = (V == 21 || (!L4 && V != 45)) ? 2 : 0;
+        const uint32_t fix = window_issue<kWinAux>(rs, frames_bytes, fr, lane, d, addr);
         window_commit(W, rs, frames_bytes, d, addr, fix, lane);
     }
     EdgeLines X{false, 0u, 0u, 0u};
@@ -886,6 +892,7 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 42: return RPKT_V(42);
         case 43: return RPKT_V(43);
         case 44: return RPKT_V(44);
+        case 45: return RPKT_V(45);
         case 10:
             return launch(copy_ref_kernel<4, false>, dim3(2048), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
