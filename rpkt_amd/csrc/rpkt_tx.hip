@@ -4,6 +4,10 @@
 
 namespace {
 
+#ifndef RPKT_BUILD_WIN_AUX
+#define RPKT_BUILD_WIN_AUX 0     // cache policy of build_kernel's window loads (2 = nt)
+#endif
+
 // ---- TX side: header build and the loopback_rx forward rewrite ----
 // Both compose the fixed header bytes of a frame from an rpkt_rec_t in the frame's
 // LDS slot (slot byte x <-> absolute (off & ~15) + x, as for the parse window) and
@@ -211,7 +215,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
-        const uint32_t fix = window_issue(rs, fb, fr, lane, d, addr);
+        const uint32_t fix = window_issue<RPKT_BUILD_WIN_AUX>(rs, fb, fr, lane, d, addr);
         load_records_tile(recs, p0, n, W, lane, w);             // window loads in flight
         window_commit(W, rs, fb, d, addr, fix, lane);
     }
