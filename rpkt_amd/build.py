@@ -24,6 +24,8 @@ GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
             "rpkt_coll.hip")]
 GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
+# units compiled a second time with other defines (same source: same unit hash)
+SECOND_COMPILES = [("rpkt_tx.hip", "rpkt_tx_w64.o", ["-DRPKT_WIN=64", "-DRPKT_TX_W64"])]
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
 HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 
@@ -67,10 +69,11 @@ def build_gpu(force=False, extra=()):
     flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
              '-DRPKT_SRC_HASH="%s"' % source_hash(), '-DRPKT_UNIT_HASHES="%s"' % unit_hashes()] + \
         list(extra)
-    objs = [os.path.join(OUT, os.path.basename(f).replace(".hip", ".o")) for f in GPU_SRC]
-    with ThreadPoolExecutor(max_workers=len(GPU_SRC)) as ex:
-        list(ex.map(lambda so: subprocess.check_call(flags + ["-c", "-o", so[1], so[0]]),
-                    zip(GPU_SRC, objs)))
+    jobs = [(f, os.path.join(OUT, os.path.basename(f).replace(".hip", ".o")), []) for f in GPU_SRC]
+    jobs += [(os.path.join(HERE, "csrc", src), os.path.join(OUT, obj), d) for src, obj, d in SECOND_COMPILES]
+    objs = [o for _, o, _ in jobs]
+    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        list(ex.map(lambda j: subprocess.check_call(flags + j[2] + ["-c", "-o", j[1], j[0]]), jobs))
     # librccl.so.1 by soname: under torch it resolves to the RCCL torch already loaded
     subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", GPU_LIB] + objs +
                           ["-L" + ROCM_LIB, "-lrccl"])

@@ -47,7 +47,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;            // lanes per wavefront (CDNA)
 constexpr int kWavesPerBlock = 4;    // 256-thread workgroups
-constexpr int kWin = 128;            // header window bytes per frame in LDS
+#ifndef RPKT_WIN
+#define RPKT_WIN 128
+#endif
+// header window bytes per frame in LDS: 128, or 64 in the TX unit's second compile
+// (rpkt_tx.hip with RPKT_TX_W64) for strided batches of frames within 64 bytes
+constexpr int kWin = RPKT_WIN;
 constexpr int kWinChunks = kWin / 16;
 constexpr int kSlot = kWin + 4;      // LDS slot stride: 33 dwords, so lane-strided
                                      // reads of the 64 slots hit 32 distinct banks
@@ -58,8 +63,10 @@ constexpr uint32_t kSplitStreamBytes = 65536;  // tile stream above which edge l
 constexpr uint32_t kEdgeWindowBytes = 32768;   // tile stream above which the window phase
                                                // sums the edge lines (edge_lines_window)
 
-struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit a CU
-    uint8_t  win[kWave * kSlot];     // header windows, slot stride 132 B
+// the window area also stages a tile's 64 records (stride 21 dwords)
+constexpr int kWinArea = kWave * kSlot > kWave * 21 * 4 ? kWave * kSlot : kWave * 21 * 4;
+struct WaveScratch {                 // 9744 B per wave at kWin 128: 4 waves x 4 blocks fit a CU
+    uint8_t  win[kWinArea];          // header windows, slot stride kWin + 4
     uint32_t s[kWave];               // window phase: frame offset; stream: range start
     uint32_t e[kWave];               // window phase: frame length; stream: range end
     uint32_t pref[kWave + 1];        // stream: exclusive prefix of chunk counts
@@ -67,7 +74,7 @@ struct WaveScratch {                 // 9744 B per wave: 4 waves x 4 blocks fit 
     uint32_t last[kWave];            // stream: scan value at a range's last chunk
 };
 static_assert(sizeof(WaveScratch) * kWavesPerBlock * 4 <= 160 * 1024, "4 blocks per CU");
-static_assert((64 * 21 + 705) * 4 <= 64 * 132, "chain scratch fits the window area");
+static_assert(kWin != 128 || (64 * 21 + 705) * 4 <= kWinArea, "chain scratch fits the window area");
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

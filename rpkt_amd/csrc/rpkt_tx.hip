@@ -7,6 +7,9 @@ namespace {
 #ifndef RPKT_BUILD_WIN_AUX
 #define RPKT_BUILD_WIN_AUX 0     // cache policy of build_kernel's window loads (2 = nt)
 #endif
+#ifndef RPKT_TX_W64_ON
+#define RPKT_TX_W64_ON 1         // hand short strided batches to the 64-B-window compile
+#endif
 
 // ---- TX side: header build and the loopback_rx forward rewrite ----
 // Both compose the fixed header bytes of a frame from an rpkt_rec_t in the frame's
@@ -296,8 +299,16 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
 // V: ablation variant for tools/ablate.py (0 = the product kernel; 1 = no write-back,
 // 2 = parse without the L4 sum, 3 = window + write-back of the whole frame only,
 // 4 = default-policy window loads).
+#ifndef RPKT_FWD_WAVES_W64
+#define RPKT_FWD_WAVES_W64 5     // 64-B windows: LDS allows 6 waves per SIMD; 5 -> <= 96 VGPRs
+#endif
+#ifdef RPKT_TX_W64
+#define RPKT_FWD_WAVES RPKT_FWD_WAVES_W64
+#else
+#define RPKT_FWD_WAVES 4
+#endif
 template <int V>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+__global__ __launch_bounds__(kWave * kWavesPerBlock, RPKT_FWD_WAVES)
 void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
                     uint32_t stride, uint32_t frame_len, uint32_t n, rpkt_fwd_t fwd,
                     uint8_t* __restrict__ keep) {
@@ -410,10 +421,35 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
 
 }  // namespace
 
+// This unit compiles twice: as is (128-B windows) and with RPKT_TX_W64 (RPKT_WIN 64,
+// rpkt_amd/build.py), whose entry points are the hidden *_w64 functions the first
+// compile hands strided batches of short frames to: a 64-B frame needs only a 64-B
+// window, so a wave's LDS drops from 9.7 to 6.7 KB and the block from 38.9 to 26.6 KB,
+// and the VGPRs, not the LDS, set the waves per SIMD.
+#ifdef RPKT_TX_W64
+#define RPKT_TX_FN(name) __attribute__((visibility("hidden"))) name##_w64
+#else
+#define RPKT_TX_FN(name) name
+#endif
+
 extern "C" {
 
-int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint32_t flags,
-                         uint8_t* built_dev, void* stream) {
+#ifndef RPKT_TX_W64
+int rpkt_gpu_build_batch_w64(const rpkt_batch_t*, const rpkt_rec_t*, uint32_t, uint8_t*, void*);
+int rpkt_gpu_forward_batch_w64(const rpkt_batch_t*, const rpkt_fwd_t*, uint8_t*, void*);
+int rpkt_gpu_debug_forward_variant_w64(const rpkt_batch_t*, const rpkt_fwd_t*, uint8_t*, int, void*);
+#endif
+
+#ifndef RPKT_TX_W64
+// strided, every frame within 64 bytes of its 16-B boundary: the 64-B-window compile
+static bool tx_w64_fits(const rpkt_batch_t* b, uint32_t flen) {
+    if (b->offsets_dev || b->stride == 0 || flen == 0) return false;
+    return flen + ((b->stride & 15u) ? 15u : 0u) <= 64u;
+}
+#endif
+
+int RPKT_TX_FN(rpkt_gpu_build_batch)(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
+                                     uint32_t flags, uint8_t* built_dev, void* stream) {
     if (!b || !recs_dev) return RPKT_E_INVAL;
     if (flags & ~(uint32_t)(RPKT_BUILD_IP_CSUM | RPKT_BUILD_L4_CSUM)) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
@@ -423,6 +459,10 @@ int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint
     if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)b->frames_dev & 15u) != 0)
         return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+#ifndef RPKT_TX_W64
+    if (RPKT_TX_W64_ON && tx_w64_fits(b, flen))
+        return rpkt_gpu_build_batch_w64(b, recs_dev, flags, built_dev, stream);
+#endif
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true> : build_kernel<false>;
@@ -431,8 +471,8 @@ int rpkt_gpu_build_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev, uint
                   b->stride, flen, b->n, recs_dev, flags, built_dev);
 }
 
-int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
-                           void* stream) {
+int RPKT_TX_FN(rpkt_gpu_forward_batch)(const rpkt_batch_t* b, const rpkt_fwd_t* fwd,
+                                       uint8_t* keep_dev, void* stream) {
     if (!b || !fwd || !keep_dev) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev || (fwd->n_forbid && !fwd->forbid_dev)) return RPKT_E_INVAL;
@@ -440,6 +480,10 @@ int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
     if (((uintptr_t)b->frames_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+#ifndef RPKT_TX_W64
+    if (RPKT_TX_W64_ON && tx_w64_fits(b, flen))
+        return rpkt_gpu_forward_batch_w64(b, fwd, keep_dev, stream);
+#endif
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     return launch(forward_kernel<0>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
@@ -448,10 +492,23 @@ int rpkt_gpu_forward_batch(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t
 }
 
 // Development hook (not part of include/rpkt_gpu.h): forward_kernel ablation variants.
-int rpkt_gpu_debug_forward_variant(const rpkt_batch_t* b, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
-                                   int variant, void* stream) {
+int RPKT_TX_FN(rpkt_gpu_debug_forward_variant)(const rpkt_batch_t* b, const rpkt_fwd_t* fwd,
+                                               uint8_t* keep_dev, int variant, void* stream) {
     if (!b || !fwd || !keep_dev || b->n == 0) return RPKT_E_INVAL;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+#ifndef RPKT_TX_W64
+    if (variant >= 10) {                          // the 64-B-window compile's variants
+        if (!tx_w64_fits(b, flen)) return RPKT_E_INVAL;
+        return rpkt_gpu_debug_forward_variant_w64(b, fwd, keep_dev, variant - 10, stream);
+    }
+    if (variant == 9) {                           // the product path of this compile only
+        const uint32_t per_block = kWave * kWavesPerBlock;
+        return launch(forward_kernel<0>, dim3((b->n + per_block - 1) / per_block), dim3(per_block), 0,
+                      (hipStream_t)stream, const_cast<uint8_t*>(b->frames_dev),
+                      (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, *fwd,
+                      keep_dev);
+    }
+#endif
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
 #define RPKT_FV(v)                                                                          \

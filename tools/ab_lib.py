@@ -25,9 +25,11 @@ def build_b(out_dir, extra):
     flags = [build.HIPCC, "--offload-arch=" + build.ARCH, "-O3", "-std=c++17", "-fPIC",
              '-DRPKT_SRC_HASH="ab"'] + list(extra)
     objs = []
-    for f in build.GPU_SRC:
-        o = os.path.join(out_dir, os.path.basename(f).replace(".hip", ".o"))
-        subprocess.check_call(flags + ["-c", "-o", o, f])
+    jobs = [(f, os.path.basename(f).replace(".hip", ".o"), []) for f in build.GPU_SRC]
+    jobs += [(os.path.join(build.HERE, "csrc", f), o, d) for f, o, d in build.SECOND_COMPILES]
+    for f, o, d in jobs:
+        o = os.path.join(out_dir, o)
+        subprocess.check_call(flags + d + ["-c", "-o", o, f])
         objs.append(o)
     lib = os.path.join(out_dir, "librpkt_gpu.so")
     subprocess.check_call([build.HIPCC, "--offload-arch=" + build.ARCH, "-shared", "-fPIC",
