@@ -136,3 +136,36 @@ def test_forward_empty_forbid_and_rejects(torch):
     assert np.array_equal(keep.astype(bool), r["ip_sum"] == 0xFFFF)
     with pytest.raises(engine.RpktError):
         engine.build_batch(db, recs, flags=4)
+
+
+def strided_short(src, stride, flen):
+    """Frames of a packed batch cut or padded to flen bytes, placed at `stride`."""
+    n = src.n
+    buf = np.zeros(n * stride + 64, dtype=np.uint8)
+    lens = src.lens()
+    for i in range(n):
+        a = int(src.offsets[i])
+        k = min(int(lens[i]), flen)
+        buf[i * stride:i * stride + k] = src.frames[a:a + k]
+    return gen.HostBatch(src.config, n, 0, buf, None, stride, flen)
+
+
+@pytest.mark.parametrize("stride,flen", [(64, 64), (64, 42), (48, 48), (49, 49), (80, 64),
+                                         (64, 65), (96, 96)])
+def test_tx_short_strided_frames(torch, stride, flen):
+    """Build and forward over strided batches around the 64-B-window compile's bound
+    (frame + 16-B phase <= 64 takes it, the last two cases take the 128-B one): IMIX
+    frames (TCP and UDP) cut to flen bytes, every frame rebuilt / rewritten exactly as
+    the oracle does, no byte outside a frame touched."""
+    hb = strided_short(gen.make_batch(4, 20000, seed=stride + flen), stride, flen)
+    recs = oracle.parse_batch(hb.frames, hb.n, 3, stride=hb.stride, frame_len=hb.frame_len)
+    for flags in (1, 3):
+        check_build(torch, hb, recs, flags)
+    db = engine.DeviceBatch.from_host(hb)
+    r = as_records(engine.parse_batch(db, 3).cpu().numpy())
+    forbid = np.unique(r["ip_src"][::31])[:16].astype(np.int64)
+    keep = engine.forward_batch(db, DMAC, SMAC, engine.forbid_list(forbid))
+    o, ok = oracle.forward_batch(hb.frames, hb.n, r, DMAC, SMAC, forbid.astype(np.uint32),
+                                 stride=hb.stride, frame_len=hb.frame_len)
+    assert np.array_equal(keep.cpu().numpy(), ok)
+    assert np.array_equal(db.frames.cpu().numpy()[:o.size], o)
