@@ -10,6 +10,22 @@ namespace {
 #ifndef RPKT_TX_W64_ON
 #define RPKT_TX_W64_ON 1         // hand short strided batches to the 64-B-window compile
 #endif
+// The 64-B-window compile serves only batches where every frame lies inside its window
+// (tx_w64_fits, checked on the host before the hand-over): no frame has bytes past the
+// window, so the edge lines and the payload stream of the L4 sums are compiled out.
+#ifndef RPKT_TX_WHOLE
+#define RPKT_TX_WHOLE 1
+#endif
+#ifndef RPKT_TX_LDS_PAD
+#define RPKT_TX_LDS_PAD 0        // extra LDS per block (ablation: caps the blocks per CU)
+#endif
+#ifdef RPKT_TX_W64
+constexpr bool kWholeFrame = RPKT_TX_WHOLE;
+constexpr uint32_t kTxLdsPad = RPKT_TX_LDS_PAD;
+#else
+constexpr bool kWholeFrame = false;
+constexpr uint32_t kTxLdsPad = 0;
+#endif
 
 // ---- TX side: header build and the loopback_rx forward rewrite ----
 // Both compose the fixed header bytes of a frame from an rpkt_rec_t in the frame's
@@ -224,7 +240,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     }
     const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
     EdgeLines X{false, 0u, 0u, 0u};
-    if constexpr (L4FILL) X = edge_lines_first(rs, fb, W, lane, valid, wend, fend);
+    if constexpr (L4FILL && !kWholeFrame) X = edge_lines_first(rs, fb, W, lane, valid, wend, fend);
     wave_sync();
 
     const uint32_t ph = fr.off & 15u, len = fr.len;
@@ -269,7 +285,8 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         }
         *reinterpret_cast<uint32_t*>(slot + kWin) =
             (uint32_t)fill_l4 | ((uint32_t)(proto == 17u) << 1) | ((ph + l4) << 8);
-        const uint32_t sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
+        uint32_t sp = 0;
+        if constexpr (!kWholeFrame) sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
         const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
         if (info & 1u) {
             const uint32_t at = info >> 8;                      // slot offset of the L4 header
@@ -378,7 +395,8 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         *reinterpret_cast<uint32_t*>(slot + kWin) =
             (uint32_t)pre | (l4 << 8) | ((L.w[15] & 0xffffu) << 16);
     }
-    const uint32_t sp = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
+    uint32_t sp = 0;
+    if constexpr (!kWholeFrame) sp = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
     const uint32_t l4_sum =
         L.want_l4 ? fold16(L.pseudo + be_sum(L.l4_part + sp, L.l4_start_abs)) : 0u;
     const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
@@ -466,7 +484,7 @@ int RPKT_TX_FN(rpkt_gpu_build_batch)(const rpkt_batch_t* b, const rpkt_rec_t* re
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true> : build_kernel<false>;
-    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    return launch(k, dim3(grid), dim3(per_block), kTxLdsPad, (hipStream_t)stream,
                   const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
                   b->stride, flen, b->n, recs_dev, flags, built_dev);
 }
@@ -486,7 +504,7 @@ int RPKT_TX_FN(rpkt_gpu_forward_batch)(const rpkt_batch_t* b, const rpkt_fwd_t* 
 #endif
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(forward_kernel<0>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    return launch(forward_kernel<0>, dim3(grid), dim3(per_block), kTxLdsPad, (hipStream_t)stream,
                   const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
                   b->stride, flen, b->n, *fwd, keep_dev);
 }
@@ -503,7 +521,7 @@ int RPKT_TX_FN(rpkt_gpu_debug_forward_variant)(const rpkt_batch_t* b, const rpkt
     }
     if (variant == 9) {                           // the product path of this compile only
         const uint32_t per_block = kWave * kWavesPerBlock;
-        return launch(forward_kernel<0>, dim3((b->n + per_block - 1) / per_block), dim3(per_block), 0,
+        return launch(forward_kernel<0>, dim3((b->n + per_block - 1) / per_block), dim3(per_block), kTxLdsPad,
                       (hipStream_t)stream, const_cast<uint8_t*>(b->frames_dev),
                       (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, *fwd,
                       keep_dev);
@@ -512,7 +530,7 @@ int RPKT_TX_FN(rpkt_gpu_debug_forward_variant)(const rpkt_batch_t* b, const rpkt
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
 #define RPKT_FV(v)                                                                          \
-    launch(forward_kernel<v>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,          \
+    launch(forward_kernel<v>, dim3(grid), dim3(per_block), kTxLdsPad, (hipStream_t)stream,          \
            const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,  \
            b->stride, flen, b->n, *fwd, keep_dev)
     switch (variant) {

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--leg", default="opts5")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="distinct batches per side (default: 8 at 64 B, as bench.py)")
     args, extra = ap.parse_known_args()
     if args.build:
         return build_b(args.build, extra)
@@ -54,10 +56,13 @@ def main():
     A = engine.lib()
     B = ctypes.CDLL(os.path.abspath(args.lib_b))
     mode, cfg = args.leg.rstrip("0123456789"), int(args.leg[len(args.leg.rstrip("0123456789")):])
-    hb = gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else gen.make_batch(cfg)
-    db = engine.DeviceBatch.from_host(hb)
-    desc = db.desc()
-    recs = engine.parse_batch(db, 3)
+    R = args.rotate or (8 if cfg == 2 else 1)    # 8 x 64 MiB of frames: past the 256 MiB cache
+    hbs = [gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else
+           gen.make_batch(cfg, seed=gen.DEFAULT_SEED[cfg] + 104729 * r) for r in range(R)]
+    hb = hbs[0]
+    dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
+    descs = [d.desc() for d in dbs]
+    recss = [engine.parse_batch(d, 3) for d in dbs]
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
     P = ctypes.POINTER(engine.Batch)
@@ -67,40 +72,42 @@ def main():
     fwd.dmac[:] = [0xAC, 0xDC, 0xCA, 0x79, 0xCA, 0x86]
     fwd.smac[:] = [0xAC, 0xDC, 0xCA, 0x79, 0xE5, 0xC6]
     fwd.forbid_dev, fwd.n_forbid = forbid.data_ptr(), forbid.numel()
+    # call[name](k): launch k of a side, on batch k % R (both sides run the same sequence)
     for name, L in (("A", A), ("B", B)):
         if mode == "opts":
             L.rpkt_gpu_options_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
-            call[name] = (lambda L=L, out=out: L.rpkt_gpu_options_batch(
-                ctypes.byref(desc), recs.data_ptr(), out.data_ptr(), sp))
+            call[name] = (lambda k, L=L, out=out: L.rpkt_gpu_options_batch(
+                ctypes.byref(descs[k % R]), recss[k % R].data_ptr(), out.data_ptr(), sp))
         elif mode == "layers":
             L.rpkt_gpu_layers_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p]
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
-            call[name] = (lambda L=L, out=out: L.rpkt_gpu_layers_batch(
-                ctypes.byref(desc), out.data_ptr(), sp))
+            call[name] = (lambda k, L=L, out=out: L.rpkt_gpu_layers_batch(
+                ctypes.byref(descs[k % R]), out.data_ptr(), sp))
         elif mode == "parse":
             L.rpkt_gpu_parse_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p]
             out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
             flags = 1 if cfg == 2 else 3
-            call[name] = (lambda L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
-                ctypes.byref(desc), flags, out.data_ptr(), None, 0, sp))
+            call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
+                ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
         elif mode in ("build", "forward"):          # in place: each side its own frames
-            dbx = engine.DeviceBatch.from_host(hb)
-            dx = dbx.desc()
+            dbx = [engine.DeviceBatch.from_host(h) for h in hbs]
+            dx = [d.desc() for d in dbx]
             out = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
             keep_alive.append((dbx, dx))
             if mode == "build":
                 L.rpkt_gpu_build_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_uint32,
                                                    ctypes.c_void_p, ctypes.c_void_p]
-                call[name] = (lambda L=L, out=out, dx=dx: L.rpkt_gpu_build_batch(
-                    ctypes.byref(dx), recs.data_ptr(), 3, out.data_ptr(), sp))
+                call[name] = (lambda k, L=L, out=out, dx=dx: L.rpkt_gpu_build_batch(
+                    ctypes.byref(dx[k % R]), recss[k % R].data_ptr(), 3, out.data_ptr(), sp))
             else:
                 L.rpkt_gpu_forward_batch.argtypes = [P, ctypes.POINTER(engine.Fwd), ctypes.c_void_p,
                                                      ctypes.c_void_p]
-                call[name] = (lambda L=L, out=out, dx=dx: L.rpkt_gpu_forward_batch(
-                    ctypes.byref(dx), ctypes.byref(fwd), out.data_ptr(), sp))
-            outs[name + "_frames"] = dbx.frames
+                call[name] = (lambda k, L=L, out=out, dx=dx: L.rpkt_gpu_forward_batch(
+                    ctypes.byref(dx[k % R]), ctypes.byref(fwd), out.data_ptr(), sp))
+            for r, d in enumerate(dbx):
+                outs["%s_frames%d" % (name, r)] = d.frames
         else:
             raise SystemExit("leg %s: not wired" % args.leg)
         outs[name] = out
@@ -109,8 +116,8 @@ def main():
         for name in ("A", "B"):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            for _ in range(args.launches):
-                rc = call[name]()
+            for k in range(args.launches):
+                rc = call[name](k)
                 assert rc == 0, rc
             e1.record(st)
             torch.cuda.synchronize()
@@ -118,7 +125,7 @@ def main():
                 times[name].append(e0.elapsed_time(e1) / args.launches * 1e3)
     same = all(outs[k].cpu().numpy().tobytes() == outs["B" + k[1:]].cpu().numpy().tobytes()
                for k in outs if k.startswith("A"))
-    print(json.dumps({"leg": args.leg, "n": hb.n, "identical": same,
+    print(json.dumps({"leg": args.leg, "n": hb.n, "rotate": R, "identical": same,
                       "A_us": round(float(np.median(times["A"])), 2),
                       "B_us": round(float(np.median(times["B"])), 2)}))
 
