@@ -13,15 +13,29 @@ namespace {
 // The 64-B-window compile serves only batches where every frame lies inside its window
 // (tx_w64_fits, checked on the host before the hand-over): no frame has bytes past the
 // window, so the edge lines and the payload stream of the L4 sums are compiled out.
+// With the stream gone the kernels need 60 / 39 VGPRs and the LDS (26.6 KB per block)
+// sets the occupancy: 6 blocks (6 waves per SIMD) per CU.  Dynamic LDS caps it at
+// RPKT_TX_W64_BLOCKS: 8 rotated batches, same process, 5 blocks vs 6: build 2 41.6 vs
+// 42.6 us, forward 2 28.0 vs 28.5 us; 4 blocks 41.9 / 28.8 (profiles/r02_txw64/).
 #ifndef RPKT_TX_WHOLE
-#define RPKT_TX_WHOLE 1
+#define RPKT_TX_WHOLE 1          // 0: keep the stream code (ablation)
 #endif
-#ifndef RPKT_TX_LDS_PAD
-#define RPKT_TX_LDS_PAD 0        // extra LDS per block (ablation: caps the blocks per CU)
+#ifndef RPKT_TX_W64_BLOCKS
+#define RPKT_TX_W64_BLOCKS 5     // blocks per CU of the 64-B-window kernels (0: no cap)
 #endif
 #ifdef RPKT_TX_W64
+constexpr uint32_t kCuLds = 160 * 1024;
+__host__ __device__ constexpr uint32_t lds_pad_for(uint32_t blocks, uint32_t block_lds) {
+    // the least dynamic LDS so that blocks + 1 no longer fit a CU
+    return blocks == 0 || kCuLds / (blocks + 1) + 1 <= block_lds ? 0u
+                                                                 : kCuLds / (blocks + 1) + 1 - block_lds;
+}
 constexpr bool kWholeFrame = RPKT_TX_WHOLE;
-constexpr uint32_t kTxLdsPad = RPKT_TX_LDS_PAD;
+constexpr uint32_t kTxLdsPad =
+    lds_pad_for(RPKT_TX_W64_BLOCKS, (uint32_t)sizeof(WaveScratch) * kWavesPerBlock);
+static_assert(RPKT_TX_W64_BLOCKS == 0 ||
+              RPKT_TX_W64_BLOCKS * (sizeof(WaveScratch) * kWavesPerBlock + kTxLdsPad) <= kCuLds,
+              "the capped block count still fits a CU");
 #else
 constexpr bool kWholeFrame = false;
 constexpr uint32_t kTxLdsPad = 0;
