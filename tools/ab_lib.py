@@ -91,6 +91,21 @@ def main():
             flags = 1 if cfg == 2 else 3
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
+        elif mode == "flow":                        # flow counters over the batch's events
+            if "ev" not in outs:
+                _, ev = engine.parse_batch(dbs[0], 3 | engine.F_FLOW_EV, n_buckets=8192)
+                outs["ev"] = ev
+            ev = outs["ev"]
+            L.rpkt_gpu_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            L.rpkt_gpu_flow_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+            L.rpkt_gpu_flow_workspace_bytes.restype = ctypes.c_size_t
+            ws = torch.empty(max(16, L.rpkt_gpu_flow_workspace_bytes(hb.n, 8192)), dtype=torch.uint8,
+                             device="cuda")
+            out = torch.zeros(8193 * 4, dtype=torch.int64, device="cuda")
+            keep_alive.append(ws)
+            call[name] = (lambda k, L=L, out=out, ws=ws: L.rpkt_gpu_flow_count(
+                ev.data_ptr(), hb.n, 8192, out.data_ptr(), ws.data_ptr(), sp))
         elif mode in ("build", "forward"):          # in place: each side its own frames
             dbx = [engine.DeviceBatch.from_host(h) for h in hbs]
             dx = [d.desc() for d in dbx]
