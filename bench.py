@@ -243,7 +243,7 @@ def pmc_traffic_tx(leg):
             t = json.load(fh)
     except (OSError, ValueError):
         return None, None
-    unit = {"build": "tx", "forward": "tx", "opts": "walks", "layers": "walks",
+    unit = {"build": "tx", "forward": "tx", "opts": "walks", "optsc": "walks", "layers": "walks",
             "fields": "fields"}[leg.rstrip("0123456789")]
     if leg not in t["legs"] or not same_unit(t.get("engine_build"), unit):
         return None, None
@@ -499,6 +499,21 @@ FIELD_LEG = [("ETHER_ETHERFRAME", "dst_addr"), ("ETHER_ETHERFRAME", "src_addr"),
              ("TCP_TCP", "seq_num"), ("VXLAN_VXLAN", "vni")]
 
 
+TX_MODES = ("build", "forward", "opts", "optsc", "layers", "fields")
+
+
+def tx_legs(spec):
+    """--tx "build2,optsc5,..." -> [(leg, mode, config)]; an unknown leg is an error."""
+    out = []
+    for leg in [x.strip() for x in spec.split(",") if x.strip()]:
+        mode = leg.rstrip("0123456789")
+        if mode not in TX_MODES or mode == leg:
+            raise SystemExit("bench.py: unknown --tx leg %r (modes %s + a config number)"
+                             % (leg, ", ".join(TX_MODES)))
+        out.append((leg, mode, int(leg[len(mode):])))
+    return out
+
+
 def run_tx(cfg, mode, args, rank, world):
     """TX side: rpkt_gpu_build_batch (headers + both checksums filled, the
     rpkt_build.rs path) or rpkt_gpu_forward_batch (loopback_rx rewrite) over a
@@ -517,7 +532,9 @@ def run_tx(cfg, mode, args, rank, world):
                for r in range(R)]
     dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
     recs = [engine.parse_batch(db, 3) for db in dbs]
-    outs = [torch.empty(hb.n * (64 if mode in ("opts", "layers") else 1), dtype=torch.uint8,
+    # optsc: the option walks located by compact records (rpkt_gpu_options_batch_compact)
+    recs16 = [engine.parse_batch_compact(db, 3) for db in dbs] if mode == "optsc" else None
+    outs = [torch.empty(hb.n * (64 if mode in ("opts", "optsc", "layers") else 1), dtype=torch.uint8,
                         device="cuda") for hb in hbs]
     if mode == "fields":                       # the walk once, outside the timed region
         lays = [engine.layers_batch(db) for db in dbs]
@@ -535,6 +552,8 @@ def run_tx(cfg, mode, args, rank, world):
             engine.build_batch(dbs[j], recs[j], 3, built=outs[j], stream=stream)
         elif mode == "opts":
             engine.options_batch(dbs[j], recs[j], opts=outs[j], stream=stream)
+        elif mode == "optsc":
+            engine.options_batch(dbs[j], recs16[j], opts=outs[j], stream=stream, compact=True)
         elif mode == "layers":
             engine.layers_batch(dbs[j], out=outs[j], stream=stream)
         elif mode == "fields":
@@ -574,12 +593,12 @@ def run_tx(cfg, mode, args, rank, world):
                   for q in reqs]
         got = sum(int(((pm >> r) & 1).sum()) * nb for r, nb in enumerate(nbytes))
         alg = hbs[0].n * (64 + 8 * len(reqs) + 4) + got
-    elif mode == "opts":                       # records + option slices read, 64 B written
+    elif mode in ("opts", "optsc"):            # records + option slices read, 64 B written
         ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
         slices = np.where(ip_parsed, r["l4_off"].astype(np.int64) - r["l3_off"] - 20, 0) + \
             np.where(tcp, r["payload_off"].astype(np.int64) - r["l4_off"] - 20, 0)
-        alg = hbs[0].n * (REC_BYTES + 64) + int(slices.sum())
+        alg = hbs[0].n * ((REC16_BYTES if mode == "optsc" else REC_BYTES) + 64) + int(slices.sum())
     else:
         kept = outs[0].cpu().numpy().astype(bool)
         alg = int(lens.sum()) + hbs[0].n + int(kept.sum()) * 42
@@ -595,6 +614,8 @@ def run_tx(cfg, mode, args, rank, world):
                      "fill" if mode == "build" else
                      "options: Ipv4OptionsIter + TcpOptionsIter walks of a parsed batch"
                      if mode == "opts" else
+                     "options from compact 16-B records (rpkt_gpu_options_batch_compact)"
+                     if mode == "optsc" else
                      "layers: pktfmt-derived protocol walk (captures mix, fuzzed)"
                      if mode == "layers" else
                      "fields: %d pktfmt getters per frame over the layer walk (captures mix)"
@@ -616,9 +637,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="all-cores CPU leg threads (0 = every usable host thread)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tx", default="build2,build3,forward2,opts5,layers9,fields9",
+    ap.add_argument("--tx", default="build2,build3,forward2,opts5,optsc5,layers9,fields9",
                     help="legs beyond the parse reported under 'extra' (build<cfg>, "
-                         "forward<cfg>, opts<cfg>)")
+                         "forward<cfg>, opts<cfg>, optsc<cfg> (compact records), layers9, "
+                         "fields9)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--dist-backend", default="nccl",
@@ -673,9 +695,8 @@ def main():
     for c in [int(x) for x in args.also.split(",") if x.strip()]:
         if c != args.config:
             extra["config%d" % c] = run_config(c, args, rank, world, cpu=want_cpu)
-    for leg in [x.strip() for x in args.tx.split(",") if x.strip()]:
-        mode = next(m for m in ("build", "forward", "opts", "layers", "fields") if leg.startswith(m))
-        extra["tx_" + leg] = run_tx(int(leg[len(mode):]), mode, args, rank, world)
+    for leg, mode, cfg in tx_legs(args.tx):
+        extra["tx_" + leg] = run_tx(cfg, mode, args, rank, world)
     for c in [int(x) for x in args.compact.split(",") if x.strip()]:
         extra["config%d_compact" % c] = run_config(c, args, rank, world, compact=True)
     if want_cpu and not args.no_config1:

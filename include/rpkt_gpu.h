@@ -385,6 +385,13 @@ typedef struct rpkt_opts {
 int rpkt_gpu_options_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
                            rpkt_opts_t* opts_dev, void* stream);
 
+/* The same walks located by compact records (rpkt_gpu_parse_batch_compact on the same
+ * batch): status, ip_protocol, l3_off, l4_off and payload_off (the TCP slice's end)
+ * are all the walks read, so the 16-B record serves as well as the 80-B one and the
+ * results are identical.  recs_dev n * 16 B, opts_dev n * 64 B, both 16-byte aligned. */
+int rpkt_gpu_options_batch_compact(const rpkt_batch_t* batch, const rpkt_rec16_t* recs_dev,
+                                   rpkt_opts_t* opts_dev, void* stream);
+
 /* ---- Protocol layer walk ---------------------------------------------------------- */
 
 /* The protocol stack of each frame, walked with the header views of every protocol

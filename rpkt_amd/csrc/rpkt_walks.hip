@@ -102,10 +102,14 @@ __device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
     return true;
 }
 
+// C16: the records are rpkt_rec16_t (16 B: one coalesced dwordx4 per lane) instead of
+// rpkt_rec_t (80 B, staged through LDS); the walks need status, IP protocol, l3, l4 and
+// the TCP data offset (payload_off - l4 for a TCP frame that parsed OK), which both hold.
+template <bool C16>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
-                    uint32_t n, const rpkt_rec_t* __restrict__ recs, rpkt_opts_t* __restrict__ opts) {
+                    uint32_t n, const void* __restrict__ recs_any, rpkt_opts_t* __restrict__ opts) {
     __shared__ __attribute__((aligned(16))) OptScratch scratch[kWavesPerBlock];
     // the option-type rules of both iterators (a per-lane type: LDS, not a switch)
     __shared__ uint8_t rules[2][256];
@@ -125,9 +129,18 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
     const Frame fr = spans.get(i);
 
-    // records of the tile (coalesced), keep the four words the walks need
-    uint32_t w0, w8, w14, w16;
-    {
+    // records of the tile (coalesced): status, IP protocol, l3 / l4 offsets, TCP doff
+    uint32_t status, proto, l3, l4, doff4;
+    if constexpr (C16) {
+        const u32x4* in = reinterpret_cast<const u32x4*>(recs_any);
+        const u32x4 r = i < n ? __builtin_nontemporal_load(&in[i]) : u32x4{0u, 0u, 0u, 0u};
+        status = r.x & 0xffu;                            // rpkt_rec16_t, include/rpkt_gpu.h
+        proto = (r.x >> 16) & 0xffu;
+        l3 = r.y & 0xffffu;
+        l4 = r.y >> 16;
+        doff4 = (r.z & 0xffffu) - l4;                    // payload_off - l4: TCP, status OK
+    } else {
+        const rpkt_rec_t* recs = reinterpret_cast<const rpkt_rec_t*>(recs_any);
         const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
         const u32x4* in = reinterpret_cast<const u32x4*>(recs + p0);
         u32x4 v[5];
@@ -148,18 +161,19 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             d[3] = v[k].w;
         }
         wave_sync();
-        w0 = st[lane * 21 + 0];
-        w8 = st[lane * 21 + 8];
-        w14 = st[lane * 21 + 14];
-        w16 = st[lane * 21 + 16];
+        const uint32_t w0 = st[lane * 21 + 0], w8 = st[lane * 21 + 8];
+        const uint32_t w14 = st[lane * 21 + 14], w16 = st[lane * 21 + 16];
         wave_sync();
+        status = w0 & 0xffu;
+        proto = (w8 >> 8) & 0xffu;
+        l3 = w16 & 0xffffu;
+        l4 = w16 >> 16;
+        doff4 = ((w14 >> 12) & 0xfu) * 4u;
     }
-    const uint32_t status = w0 & 0xffu;
     const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
-    const bool tcp = status == RPKT_S_OK && ((w8 >> 8) & 0xffu) == 6u;
-    const uint32_t l3 = w16 & 0xffffu, l4 = w16 >> 16;
+    const bool tcp = status == RPKT_S_OK && proto == 6u;
     const uint32_t ip_lo = l3 + 20u, ip_hi = ip_parsed ? l4 : ip_lo;
-    const uint32_t t_lo = l4 + 20u, t_hi = tcp ? l4 + ((w14 >> 12) & 0xfu) * 4u : t_lo;
+    const uint32_t t_lo = l4 + 20u, t_hi = tcp ? l4 + doff4 : t_lo;
     // option bytes needed: [lo, hi) of the frame (both slices); chunks outside it skip
     const uint32_t need_lo = ip_hi > ip_lo ? ip_lo : t_lo;
     const uint32_t need_hi = t_hi > t_lo ? t_hi : ip_hi;
@@ -894,9 +908,25 @@ int rpkt_gpu_options_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(options_kernel, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    return launch(options_kernel<false>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
-                  recs_dev, opts_dev);
+                  (const void*)recs_dev, opts_dev);
+}
+
+int rpkt_gpu_options_batch_compact(const rpkt_batch_t* b, const rpkt_rec16_t* recs_dev,
+                                   rpkt_opts_t* opts_dev, void* stream) {
+    if (!b || !recs_dev || !opts_dev) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(options_kernel<true>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+                  b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
+                  (const void*)recs_dev, opts_dev);
 }
 
 int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void* stream) {

@@ -51,7 +51,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
            "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch",
            "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
-           "rpkt_gpu_parse_batch_compact"]
+           "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact"]
 
 _lib = None
 
@@ -108,6 +108,9 @@ def lib():
         L.rpkt_gpu_options_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_options_batch.restype = ctypes.c_int
+        L.rpkt_gpu_options_batch_compact.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_options_batch_compact.restype = ctypes.c_int
         L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.rpkt_gpu_layers_batch.restype = ctypes.c_int
@@ -379,16 +382,19 @@ def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None):
     return keep
 
 
-def options_batch(batch, recs, opts=None, stream=None):
+def options_batch(batch, recs, opts=None, stream=None, compact=False):
     """rpkt_gpu_options_batch: IPv4 and TCP option walks of a parsed batch
-    (recs from parse_batch); returns the uint8 tensor of n * 64-byte rpkt_opts_t."""
+    (recs from parse_batch, or from parse_batch_compact with compact=True:
+    rpkt_gpu_options_batch_compact); returns the uint8 tensor of n * 64-byte rpkt_opts_t."""
     torch = _torch()
+    if recs.numel() != batch.n * (REC16_BYTES if compact else REC_BYTES):
+        raise RpktError("records: %d bytes for %d frames" % (recs.numel(), batch.n))
     if opts is None:
         opts = torch.empty(batch.n * OPTS_BYTES, dtype=torch.uint8, device=batch.frames.device)
     d = batch.desc()
-    rc = lib().rpkt_gpu_options_batch(ctypes.byref(d), recs.data_ptr(), opts.data_ptr(),
-                                      _stream_ptr(stream))
-    _check(rc, "rpkt_gpu_options_batch")
+    fn = lib().rpkt_gpu_options_batch_compact if compact else lib().rpkt_gpu_options_batch
+    rc = fn(ctypes.byref(d), recs.data_ptr(), opts.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_options_batch_compact" if compact else "rpkt_gpu_options_batch")
     return opts
 
 

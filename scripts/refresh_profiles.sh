@@ -12,3 +12,4 @@ for c in 2 3; do
 done
 bash "$R/scripts/profile.sh" walks 2 --tx layers9,opts5,forward2,build2,fields9
 bash "$R/scripts/profile.sh" build3 2 --tx build3
+bash "$R/scripts/profile.sh" optsc5 2 --tx optsc5

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -21,3 +23,18 @@ def test_usable_cpus_within_affinity():
     import bench
     n = bench.usable_cpus()
     assert 1 <= n <= len(os.sched_getaffinity(0)) <= (os.cpu_count() or n)
+
+
+def test_tx_leg_names():
+    """Every default --tx leg parses to a known mode and config (optsc before opts)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    legs = bench.tx_legs("build2,build3,forward2,opts5,optsc5,layers9,fields9")
+    assert [(m, c) for _, m, c in legs] == [("build", 2), ("build", 3), ("forward", 2), ("opts", 5),
+                                           ("optsc", 5), ("layers", 9), ("fields", 9)]
+    with pytest.raises(SystemExit):
+        bench.tx_legs("nope2")
+    with pytest.raises(SystemExit):
+        bench.tx_legs("opts")
+    ap_default = [a for a in open(bench.__file__).read().split("\n") if '"--tx", default=' in a][0]
+    bench.tx_legs(ap_default.split('default="')[1].split('"')[0])

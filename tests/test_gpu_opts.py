@@ -1,5 +1,6 @@
 """GPU parity of rpkt_gpu_options_batch (TcpOptionsIter / Ipv4OptionsIter) against
-oracle/rpkt_oracle_opts.c, bit-exact, on the reference captures and full batches."""
+oracle/rpkt_oracle_opts.c, bit-exact, on the reference captures and full batches;
+every case also walks from compact records (rpkt_gpu_options_batch_compact)."""
 import os
 
 import numpy as np
@@ -27,18 +28,21 @@ def gpu_opts(hb):
     db = engine.DeviceBatch.from_host(hb)
     recs = engine.parse_batch(db, 3)
     o = as_opts(engine.options_batch(db, recs).cpu().numpy())
-    return o, as_records(recs.cpu().numpy())
+    r16 = engine.parse_batch_compact(db, 3)
+    oc = as_opts(engine.options_batch(db, r16, compact=True).cpu().numpy())
+    return o, oc, as_records(recs.cpu().numpy())
 
 
 def check(hb):
-    g, r = gpu_opts(hb)
+    g, gc, r = gpu_opts(hb)
     o = oracle.options_batch(hb.frames, hb.n, r, offsets=hb.offsets, stride=hb.stride,
                              frame_len=hb.frame_len)
-    if g.tobytes() != o.tobytes():
-        bad = np.nonzero(g.view(np.uint8).reshape(-1, 64) != o.view(np.uint8).reshape(-1, 64))
-        i = int(bad[0][0])
-        raise AssertionError("%d frames differ, first %d: gpu %s oracle %s" % (
-            len(np.unique(bad[0])), i, g[i], o[i]))
+    for what, x in (("full records", g), ("compact records", gc)):
+        if x.tobytes() != o.tobytes():
+            bad = np.nonzero(x.view(np.uint8).reshape(-1, 64) != o.view(np.uint8).reshape(-1, 64))
+            i = int(bad[0][0])
+            raise AssertionError("%s: %d frames differ, first %d: gpu %s oracle %s" % (
+                what, len(np.unique(bad[0])), i, x[i], o[i]))
     return g, r
 
 

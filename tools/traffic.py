@@ -64,12 +64,13 @@ TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "opt
 
 
 MODE_KERNEL = {"build": "build_kernel", "forward": "forward_kernel", "opts": "options_kernel",
+               "optsc": "options_kernel",
                "layers": "layers_kernel", "fields": "fields_kernel"}
 
 
 def main_tx(prof, out, only=None):
-    """All TX_LEGS of one profile, or (only = "build3") the one leg a profile of
-    `bench.py --tx build3` holds, merged into the existing summary of the same build."""
+    """All TX_LEGS of one profile, or (only = "build3", "optsc5") the one leg a profile
+    of `bench.py --tx <leg>` holds, merged into the existing summary of the same build."""
     def pmc(name, kname):
         v = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, name + "_counter_collection.csv"))
              if r["Kernel_Name"].startswith(kname)][5:]
@@ -97,9 +98,9 @@ def main_tx(prof, out, only=None):
                      "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024}
     res = {"engine_build": build, "legs": legs,
            "kernel_stats": rows(os.path.join(prof, "trace_kernel_stats.csv"))}
-    if only:
-        res["kernel_stats"] = old["kernel_stats"]
-        res.setdefault("kernel_stats_" + only, rows(os.path.join(prof, "trace_kernel_stats.csv")))
+    if only:                                   # keep the other single-leg profiles' stats
+        res.update({k: v for k, v in old.items() if k.startswith("kernel_stats")})
+        res["kernel_stats_" + only] = rows(os.path.join(prof, "trace_kernel_stats.csv"))
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
