@@ -373,12 +373,8 @@ __device__ __attribute__((noinline)) u32x4 lay_edge16(__amdgpu_buffer_rsrc_t rs,
 __device__ __forceinline__ void LayerWin::refill(uint32_t s) {
     const uint32_t a = (off + s) & ~15u;
     u32x4 d[kLayChunks];
-    uint32_t fix = 0;
 #pragma unroll
-    for (int k = 0; k < kLayChunks; ++k) {
-        d[k] = load16_fast(rs, a + 16u * k);
-        fix |= (uint32_t)straddles(a + 16u * k, fb) << k;
-    }
+    for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, a + 16u * k);
     uint32_t* w = reinterpret_cast<uint32_t*>(base);
 #pragma unroll
     for (int k = 0; k < kLayChunks; ++k) {
@@ -387,8 +383,11 @@ __device__ __forceinline__ void LayerWin::refill(uint32_t s) {
         w[4 * k + 2] = d[k].z;
         w[4 * k + 3] = d[k].w;
     }
-    if (__builtin_expect(fix != 0, 0)) {
-        const uint32_t k = (uint32_t)__builtin_ctz(fix);
+    // only the chunk holding the buffer's last byte can straddle its end (chunk
+    // (fb - a) / 16, when fb is not on a 16-B boundary): one test, not one per chunk
+    const uint32_t rel = fb - a;
+    if (__builtin_expect(fb > a && (rel & 15u) != 0 && rel < 16u * kLayChunks, 0)) {
+        const uint32_t k = rel >> 4;
         const u32x4 v = lay_edge16(rs, a + 16u * k, fb);
         w[4 * k] = v.x;
         w[4 * k + 1] = v.y;
