@@ -11,7 +11,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SUITES = ["tests/test_oracle_golden.py", "tests/test_oracle_chain.py",
           "tests/test_oracle_layers.py", "tests/test_oracle_fields.py",
-          "tests/test_oracle_batch.py"]
+          "tests/test_oracle_batch.py", "tests/test_oracle_fuzz_layouts.py"]
 
 
 @pytest.mark.slow
