@@ -91,6 +91,23 @@ def main():
             flags = 1 if cfg == 2 else 3
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
+        elif mode == "fields":                      # bench.py's 16 getters over the walk
+            import bench
+            from rpkt_amd import fields
+            from rpkt_amd.records import FIELD_REQ_DTYPE
+            if "lay" not in outs:
+                outs["lay"] = engine.layers_batch(dbs[0])
+            lay = outs["lay"]
+            reqs = np.ascontiguousarray(fields.requests(bench.FIELD_LEG), dtype=FIELD_REQ_DTYPE)
+            keep_alive.append(reqs)
+            L.rpkt_gpu_fields_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            out = torch.zeros((hb.n, reqs.size), dtype=torch.int64, device="cuda")
+            pres = torch.zeros(hb.n, dtype=torch.int32, device="cuda")
+            outs[name + "_present"] = pres
+            call[name] = (lambda k, L=L, out=out, pres=pres, reqs=reqs: L.rpkt_gpu_fields_batch(
+                ctypes.byref(descs[0]), lay.data_ptr(), reqs.ctypes.data_as(ctypes.c_void_p),
+                reqs.size, out.data_ptr(), pres.data_ptr(), sp))
         elif mode == "flow":                        # flow counters over the batch's events
             if "ev" not in outs:
                 _, ev = engine.parse_batch(dbs[0], 3 | engine.F_FLOW_EV, n_buckets=8192)
