@@ -727,6 +727,41 @@ __device__ __forceinline__ int lay_next(const LayHdr& H, const LayTable& T, uint
     return nx;
 }
 
+// Every walk starts with the Ethernet group (EtherGroup::group_parse,
+// ether/generated.rs:287-302): the table interpreter's first step, specialised.  A
+// frame's first step is taken with the frame (when the lane takes it from the pool),
+// so the general loop runs one iteration less per frame.  Same results as walk_group +
+// lay_next on group RPKT_G_ETHER at s = 0 (the table's Ether rows: members EtherFrame,
+// EtherType >= 0x0600, and EtherDot3Frame, length field <= 1500 trimmed as payload_len;
+// 14 header bytes; then the EtherType dispatch or LLC).  Returns the stop code (0: go on).
+#ifndef RPKT_LAY_ETHER_FIRST
+#define RPKT_LAY_ETHER_FIRST 1
+#endif
+__device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const LayTable& T,
+                                               uint32_t len, uint32_t (&o)[16], uint32_t& s,
+                                               uint32_t& e, uint32_t& nl, int& g) {
+    const uint32_t et = hdr_be16(H, 12);
+    const bool ef = et >= 0x0600u, d3 = et <= 1500u;
+    const bool ok = (len >= 14u) & (ef | d3) & !(d3 & (et + 14u > len));
+    const uint32_t p = ef ? (uint32_t)RPKT_P_ETHER_ETHERFRAME : (uint32_t)RPKT_P_ETHER_ETHERDOT3FRAME;
+    const uint32_t E = T.et[et_slot(et)];
+    int nx = ((E >> 8) == et && et != 0x6558u) ? (int)(E & 0xffu) : kNextUnknown;
+    nx = ef ? nx : RPKT_G_LLC;
+    const bool unk = ok && nx == kNextUnknown;
+    const uint32_t stop = !ok ? (uint32_t)RPKT_L_ERR : unk ? (uint32_t)RPKT_L_UNKNOWN : 0u;
+    nl = ok ? 1u : 0u;
+    e = ok && d3 ? 14u + et : len;
+    s = ok ? 14u : 0u;
+    o[4] = ok ? p : 0u;
+    o[0] = nl | (stop << 8) | ((unk ? p : 0u) << 24);
+    o[1] = s;
+    o[2] = e - s;
+    o[3] = unk ? et : 0u;
+    g = nx;
+    H = lay_hdr(Wn, s, ok);
+    return stop;
+}
+
 // Lane L of a wave walks frames base + L + 64 k, k = 0 .. F-1, one after the other: a
 // walk's depth varies from frame to frame (the capture mix: 2.6 layers on average, a
 // wave's deepest lane 6.8), and a wave runs until its deepest lane ends, so a lane
@@ -804,9 +839,16 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     uint32_t s = 0, e = fr[0].len, nl = 0;
     int g = RPKT_G_ETHER;
     LayHdr H = lay_hdr(Wn, 0u, false);                      // in the staged window
+    // DYN: a frame's first (Ethernet) step is taken with the frame; pend holds the stop
+    // code of a frame that ended there, stored by the next iteration
+    constexpr bool kEth = DYN && RPKT_LAY_ETHER_FIRST;
+    uint32_t pend = 0;
+    if constexpr (kEth) {
+        if (active) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
+    }
     while (__ballot(active)) {
-        uint32_t stop = 0;
-        if (active) {
+        uint32_t stop = pend;
+        if (active && !pend) {
             uint32_t hl = 0, end = 0, rule = 0;
             const int p = walk_group(Wn, H, T, (uint32_t)g, s, e, hl, end, rule);
             const bool ok = p >= 0;
@@ -872,9 +914,11 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 for (int k = 0; k < 16; ++k) o[k] = 0;
                 s = 0, e = f.len, nl = 0, g = RPKT_G_ETHER;
                 Wn.off = f.off;
+                pend = 0;
                 if (active) {
                     Wn.refill(0u);
                     H = lay_hdr(Wn, 0u, false);
+                    if constexpr (kEth) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
                 }
             }
             if constexpr (DYN) taken += (uint32_t)__builtin_popcountll(sm);
