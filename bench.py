@@ -27,6 +27,7 @@ counters with rpkt_gpu_flow_reduce (RCCL).  The timed region is bracketed by
 barrier + synchronize and the max over ranks is reported.
 """
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -468,6 +469,8 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
         out["flow_pkts_total"] = int(c[:, 0].sum())
         # every launch (warmup included) added its shard's frames to the counters
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
+    if cfg == 2 and not compact:
+        out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
     if cpu and rank == 0 and not compact:
         g = as_records(recs[0].cpu().numpy())
         if cfg in gen.CHAINED:
@@ -479,6 +482,51 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
     del dbs, recs
     torch.cuda.empty_cache()
     return out
+
+
+def copy_ceiling(dbs, recs, steps):
+    """Measured device-to-device copy ceilings beside config 2, same
+    stream and event timing as the parse: (1) a grid-stride copy kernel moving config 2's
+    own bytes (the 8 rotated 64 MiB frame buffers read, 80 MiB of records written:
+    rpkt_gpu_debug_variant 13, tools/ablate.py's v13); (2) hipMemcpyAsync device to
+    device of 1 GiB (torch copy_), read + written bytes counted."""
+    L = engine.lib()
+    L.rpkt_gpu_debug_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    L.rpkt_gpu_debug_variant.restype = ctypes.c_int
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    descs = [db.desc() for db in dbs]
+    R = len(dbs)
+
+    def timed(fn, k):
+        for j in range(max(4, R)):
+            fn(j)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for j in range(k):
+            fn(j)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k / 1e3                     # seconds per launch
+
+    def mix(j):
+        rc = L.rpkt_gpu_debug_variant(ctypes.byref(descs[j % R]), 1, recs[j % R].data_ptr(), 13, sp)
+        if rc:
+            raise engine.RpktError("copy reference: rc %d" % rc)
+    t_mix = timed(mix, max(steps, 2 * R))
+    mix_bytes = dbs[0].frames.numel() + recs[0].numel()
+    a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    t_d2d = timed(lambda j: b.copy_(a), 10)
+    del a, b
+    return {"same_mix_copy": {"gb_per_s": round(mix_bytes / t_mix / 1e9, 1),
+                              "us": round(t_mix * 1e6, 2), "bytes": int(mix_bytes),
+                              "what": "grid-stride copy of config 2's bytes: 64 MiB frames read, "
+                                      "80 MiB records written, 8 rotated batches"},
+            "d2d_memcpy": {"gb_per_s": round(2 * (1 << 30) / t_d2d / 1e9, 1),
+                           "us": round(t_d2d * 1e6, 1), "bytes": 2 * (1 << 30),
+                           "what": "hipMemcpyAsync device to device, 1 GiB (read + write)"}}
 
 
 FORBID_IPS = ["192.168.5.%d" % k for k in range(3, 11)]    # loopback_rx.rs:42-51
@@ -732,7 +780,8 @@ def main():
             "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                           for kk, vv in v.items()} for k, v in extra.items()},
         }
-        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_pkts_total", "flow_pkts_expected"):
+        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_pkts_total", "flow_pkts_expected",
+                  "copy_ceiling"):
             if k in main_res:
                 line[k] = main_res[k]
         print(json.dumps(line), flush=True)
