@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+OUT=gpurun_out/ab_pre
+mkdir -p $OUT
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_layers.py tests/test_gpu_fuzz_layouts.py -x -q --timeout 120 --timeout-method thread \
+    > $OUT/tests.log 2>&1 || exit 1
+for leg in layers9 layers2 layers5; do
+  timeout -k 10 200 python3 -u tools/ab_lib.py rpkt_amd/_build_nopre/librpkt_gpu.so --leg $leg --rounds 8 --launches 20 \
+    > $OUT/ab_$leg.log 2>&1 || exit 1
+done
