@@ -603,9 +603,15 @@ constexpr uint32_t kFlowMaxPerBlock = 32768;
 constexpr uint32_t kFlowMinBlocks = 256;
 constexpr int kFlowUnroll = 8;
 
+// at least 16384 events per slab: below that the slabs' fixed cost (each holds every
+// bucket, written once and read by the reduce) outweighs spreading the atomics over
+// more CUs (1M events: 256 slabs 21.4 us, 128 17.3, 64 14.8; profiles/r02_ab_flow_small)
+#ifndef RPKT_FLOW_MIN_PER_BLOCK
+#define RPKT_FLOW_MIN_PER_BLOCK 16384
+#endif
 __host__ __device__ inline uint32_t flow_blocks(uint32_t n) {
     uint32_t b = (n + kFlowMaxPerBlock - 1) / kFlowMaxPerBlock;
-    uint32_t m = (n + kFlowThreads - 1) / kFlowThreads;   // >= one event per thread
+    uint32_t m = (n + RPKT_FLOW_MIN_PER_BLOCK - 1) / RPKT_FLOW_MIN_PER_BLOCK;   // slabs of >= 16384
     uint32_t want = kFlowMinBlocks < m ? kFlowMinBlocks : m;
     return b > want ? b : (want ? want : 1);
 }

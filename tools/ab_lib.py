@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--leg", default="opts5")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--n", type=int, default=0, help="frames per batch (default: the config's)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches per side (default: 8 at 64 B, as bench.py)")
     args, extra = ap.parse_known_args()
@@ -58,7 +59,8 @@ def main():
     mode, cfg = args.leg.rstrip("0123456789"), int(args.leg[len(args.leg.rstrip("0123456789")):])
     R = args.rotate or (8 if cfg == 2 else 1)    # 8 x 64 MiB of frames: past the 256 MiB cache
     hbs = [gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else
-           gen.make_batch(cfg, seed=gen.DEFAULT_SEED[cfg] + 104729 * r) for r in range(R)]
+           gen.make_batch(cfg, args.n or None, seed=gen.DEFAULT_SEED[cfg] + 104729 * r)
+           for r in range(R)]
     hb = hbs[0]
     dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
     descs = [d.desc() for d in dbs]
