@@ -740,7 +740,11 @@ __device__ __forceinline__ int lay_next(const LayHdr& H, const LayTable& T, uint
 __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const LayTable& T,
                                                uint32_t len, uint32_t (&o)[16], uint32_t& s,
                                                uint32_t& e, uint32_t& nl, int& g) {
-    const uint32_t et = hdr_be16(H, 12);
+    // the length / EtherType field straight from the slot, and the next header (at 14,
+    // used only if the walk goes on) read at once: one LDS round trip after the refill
+    const uint32_t y = 12u + Wn.bias, a = y & ~3u;
+    const uint32_t et = be16_lo(align_bytes(lds32(Wn.base, a + 4u), lds32(Wn.base, a), y & 3u));
+    H = lay_hdr(Wn, 14u, false);
     const bool ef = et >= 0x0600u, d3 = et <= 1500u;
     const bool ok = (len >= 14u) & (ef | d3) & !(d3 & (et + 14u > len));
     const uint32_t p = ef ? (uint32_t)RPKT_P_ETHER_ETHERFRAME : (uint32_t)RPKT_P_ETHER_ETHERDOT3FRAME;
@@ -758,7 +762,6 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
     o[2] = e - s;
     o[3] = unk ? et : 0u;
     g = nx;
-    H = lay_hdr(Wn, s, ok);
     return stop;
 }
 
@@ -917,8 +920,8 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 pend = 0;
                 if (active) {
                     Wn.refill(0u);
-                    H = lay_hdr(Wn, 0u, false);
                     if constexpr (kEth) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
+                    else H = lay_hdr(Wn, 0u, false);
                 }
             }
             if constexpr (DYN) taken += (uint32_t)__builtin_popcountll(sm);
