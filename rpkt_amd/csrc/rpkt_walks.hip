@@ -775,6 +775,9 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
 // taking the next untaken frame when its walk ends (82.9 -> 68.7 us on the capture
 // mix vs four fixed frames per lane, profiles/r02_fwd/ablate_layers_c9.log)
 constexpr int kLayFrames = 4;
+#ifndef RPKT_LAY_BLOCK_POOL
+#define RPKT_LAY_BLOCK_POOL 1    // 0: one pool per wave
+#endif
 
 template <int F, bool DYN = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
@@ -786,12 +789,19 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     // per-lane (divergent) loads; from LDS they cost tens of cycles instead of a
     // global-memory round trip per dependent lookup
     __shared__ __attribute__((aligned(16))) LayTable T;
+    // DYN with block pooling: the block's 4 waves share one pool of 4 x 64 F frames
+    // through an LDS counter, so they end together (per-wave pools differ by +-12 % in
+    // work on the capture mix, and a pass of waves lasts as long as its slowest)
+    constexpr bool kBlk = DYN && RPKT_LAY_BLOCK_POOL;
+    __shared__ uint32_t blk_taken;
     lay_table_fill(T);
+    if (threadIdx.x == 0) blk_taken = kWave * kWavesPerBlock;    // the waves' first tiles
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     LayScratch& W = scratch[wid];
-    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * (kWave * F);
+    const uint32_t bb = blockIdx.x * kWavesPerBlock * (kWave * F);   // the block's frames
+    const uint32_t p0 = kBlk ? bb + wid * kWave : (blockIdx.x * kWavesPerBlock + wid) * (kWave * F);
     if (p0 >= n) return;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
     const SpanSrc spans{offsets, stride, frame_len, fb, n};
@@ -894,6 +904,12 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             // busy until the pool is empty instead of after their own F frames
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+            uint32_t kbase = taken;
+            if constexpr (kBlk) {                              // every lane: full EXEC
+                uint32_t b0 = 0;
+                if (lane == 0) b0 = atomicAdd(&blk_taken, (uint32_t)__builtin_popcountll(sm));
+                kbase = (uint32_t)__shfl((int)b0, 0, kWave);
+            }
             if (stop) {
                 u32x4* dst = reinterpret_cast<u32x4*>(out + i);
 #pragma unroll
@@ -902,9 +918,9 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                                                 &dst[k]);
                 Frame f = fr[0];
                 if constexpr (DYN) {
-                    const uint32_t k = taken + rank;
-                    i = p0 + k;
-                    active = k < (uint32_t)(kWave * F) && i < n;
+                    const uint32_t k = kbase + rank;
+                    i = (kBlk ? bb : p0) + k;
+                    active = k < (uint32_t)(kWave * F * (kBlk ? kWavesPerBlock : 1)) && i < n;
                     if (active) f = spans.get(i);
                 } else {
                     fk += 1;
