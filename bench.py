@@ -469,10 +469,11 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
         out["flow_pkts_total"] = int(c[:, 0].sum())
         # every launch (warmup included) added its shard's frames to the counters
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
+    # the records of batch 0 are read back before the copy references overwrite them
+    g = as_records(recs[0].cpu().numpy()) if cpu and rank == 0 and not compact else None
     if cfg == 2 and not compact:
         out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
-    if cpu and rank == 0 and not compact:
-        g = as_records(recs[0].cpu().numpy())
+    if g is not None:
         if cfg in gen.CHAINED:
             out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds,
                                                       args.cpu_threads)
