@@ -62,9 +62,15 @@ __device__ __forceinline__ bool find_layer(const LayerView& L, uint32_t proto, u
         mm = skip ? mm >> s : mm;
         pos = skip ? pos + s : pos;
     }
-    uint32_t dw = L.off[0];
-#pragma unroll
-    for (uint32_t q = 1; q < 8; ++q) dw = (pos >> 1) == q ? L.off[q] : dw;
+    // the offset dword by a mux tree on the index bits: a chain of (index == q) selects
+    // over the array is turned by the compiler into an indexed load from a private copy
+    // of the 52-B record in scratch (written per lane and re-read, through L2 and HBM)
+    const uint32_t q = pos >> 1;
+    const bool q0 = q & 1u, q1 = q & 2u, q2 = q & 4u;
+    const uint32_t a0 = q0 ? L.off[1] : L.off[0], a1 = q0 ? L.off[3] : L.off[2];
+    const uint32_t a2 = q0 ? L.off[5] : L.off[4], a3 = q0 ? L.off[7] : L.off[6];
+    const uint32_t b0 = q1 ? a1 : a0, b1 = q1 ? a3 : a2;
+    const uint32_t dw = q2 ? b1 : b0;
     loff = (dw >> (16 * (pos & 1))) & 0xffffu;
     return (uint32_t)__builtin_popcount(m) > nth;
 }
@@ -83,12 +89,15 @@ __device__ __forceinline__ void take9(const uint32_t (&d)[3], uint32_t a, uint64
 
 // The same bytes by byte loads (bytes at or past `limit` read 0): for the rare field
 // in the last, partial dword of the buffer, which a dword load drops whole.
-__device__ __noinline__ void load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t limit,
-                                         uint64_t& hi, uint32_t& ninth) {
+// (returned by value: out-parameters of a call that is not inlined live in scratch)
+struct Bytes9 {
+    uint64_t hi;
+    uint32_t ninth;
+};
+__device__ __noinline__ Bytes9 load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t limit) {
     uint64_t h = 0;
     for (uint32_t j = 0; j < 8; ++j) h = (h << 8) | (a + j < limit ? gbyte(rs, a + j) : 0u);
-    hi = h;
-    ninth = a + 8 < limit ? gbyte(rs, a + 8) : 0u;
+    return Bytes9{h, a + 8 < limit ? gbyte(rs, a + 8) : 0u};
 }
 
 constexpr uint32_t kReqGroup = 16;     // requests whose loads are in flight together
@@ -135,7 +144,11 @@ __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
                 uint64_t hi;
                 uint32_t ninth;
                 take9(d[j], a[j], hi, ninth);
-                if (ok[j] && a[j] + 9u > full_dwords) load9_bytes(rs, a[j], frames_bytes, hi, ninth);
+                if (ok[j] && a[j] + 9u > full_dwords) {
+                    const Bytes9 b9 = load9_bytes(rs, a[j], frames_bytes);
+                    hi = b9.hi;
+                    ninth = b9.ninth;
+                }
                 // the 64 bits from the field's first bit on, then its top `bits`
                 const uint64_t w = s ? (hi << s) | (uint64_t)(ninth >> (8 - s)) : hi;
                 const uint64_t v = ok[j] ? w >> ((64u - bits) & 63u) : 0ull;
