@@ -100,30 +100,42 @@ __device__ __noinline__ Bytes9 load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a
     return Bytes9{h, a + 8 < limit ? gbyte(rs, a + 8) : 0u};
 }
 
-constexpr uint32_t kReqGroup = 16;     // requests whose loads are in flight together
+// Requests whose loads are in flight together (the ablation macro: 16 is fastest, 8 at
+// 74 VGPRs 65.0 vs 63.9 us, 4 at 60 VGPRs 177 us; profiles/r02_ab_fgroup).
+#ifndef RPKT_FIELDS_GROUP
+#define RPKT_FIELDS_GROUP 16
+#endif
+constexpr uint32_t kReqGroup = RPKT_FIELDS_GROUP;
 
 // One lane per frame: its layer record once, then the requests in groups of sixteen whose
 // 48 dword loads are issued before any is used (the request list is wave-uniform,
 // read from the kernel arguments by scalar loads; the host pads it to a multiple of
 // sixteen with requests no layer matches; their loads read offset 0, which is cheaper
-// than a wave-uniform branch around them: 99 vs 90 us).  Values are staged in LDS (frame stride
-// 2k+1 dwords: conflict-free) and stored as contiguous 8-B-per-lane rows of the
-// block's n_req x 128 outputs, non-temporal (written once, never re-read here).
+// than a wave-uniform branch around them: 99 vs 90 us).  A group's values are staged in
+// LDS (frame stride 2k+1 dwords: conflict-free) and stored as rows of up to 16 u64 per
+// frame, non-temporal (written once, never re-read here); the row index is a shift, not
+// a division by the run-time request count (70.7 -> 63.0 us same-process, profiles/r02_ab_fgroup).
 __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
     const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len, uint32_t n,
     const rpkt_layers_t* __restrict__ layers, FieldReqs reqs, uint32_t n_req,
     uint64_t* __restrict__ values, uint32_t* __restrict__ present) {
-    extern __shared__ uint32_t stage[];                  // kFieldBlock * (2 n_req + 1)
+    extern __shared__ uint32_t stage[];                  // kFieldBlock * (2 kReqGroup + 1)
     const uint32_t base = blockIdx.x * kFieldBlock, t = threadIdx.x, i = base + t;
-    const uint32_t nf = min(n - base, (uint32_t)kFieldBlock), fs = 2 * n_req + 1;
+    const uint32_t nf = min(n - base, (uint32_t)kFieldBlock);
+    constexpr uint32_t fs = 2 * kReqGroup + 1;
     const uint32_t full_dwords = frames_bytes & ~3u;
-    if (i < n) {
-        const Frame fr = frame_span(offsets, stride, frame_len, frames_bytes, i);
-        const LayerView L = load_layers(layers, i);
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
-        uint32_t mask = 0;
-        for (uint32_t r0 = 0; r0 < n_req; r0 += kReqGroup) {
+    const bool live = i < n;
+    const Frame fr = live ? frame_span(offsets, stride, frame_len, frames_bytes, i) : Frame{0u, 0u};
+    const LayerView L = live ? load_layers(layers, i) : LayerView{};
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
+    uint64_t* const out = values + (uint64_t)base * n_req;
+    uint32_t mask = 0;
+    // a group of requests at a time: loads, values into the LDS stage, then the group's
+    // values of the block's frames stored as rows of g consecutive u64 per frame (the
+    // stage holds one group, so the block's LDS does not limit the waves per CU)
+    for (uint32_t r0 = 0; r0 < n_req; r0 += kReqGroup) {
+        if (live) {
             uint32_t d[kReqGroup][3], a[kReqGroup], ok[kReqGroup];
 #pragma unroll
             for (uint32_t j = 0; j < kReqGroup; ++j) {
@@ -153,21 +165,21 @@ __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
                 const uint64_t w = s ? (hi << s) | (uint64_t)(ninth >> (8 - s)) : hi;
                 const uint64_t v = ok[j] ? w >> ((64u - bits) & 63u) : 0ull;
                 mask |= ok[j] << (r0 + j);
-                if (r0 + j < n_req) {
-                    stage[t * fs + 2 * (r0 + j)] = (uint32_t)v;
-                    stage[t * fs + 2 * (r0 + j) + 1] = (uint32_t)(v >> 32);
-                }
+                stage[t * fs + 2 * j] = (uint32_t)v;
+                stage[t * fs + 2 * j + 1] = (uint32_t)(v >> 32);
             }
         }
-        if (present) __builtin_nontemporal_store(mask, present + i);
+        __syncthreads();
+        const uint32_t g = min(kReqGroup, n_req - r0);
+        for (uint32_t e = t; e < nf * g; e += kFieldBlock) {
+            const uint32_t f = g == kReqGroup ? e / kReqGroup : e / g, r = e - f * g;
+            __builtin_nontemporal_store(
+                ((uint64_t)stage[f * fs + 2 * r + 1] << 32) | stage[f * fs + 2 * r],
+                out + (uint64_t)f * n_req + r0 + r);
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    uint64_t* out = values + (uint64_t)base * n_req;
-    for (uint32_t e = t; e < nf * n_req; e += kFieldBlock) {
-        const uint32_t f = e / n_req, r = e - f * n_req;
-        __builtin_nontemporal_store(
-            ((uint64_t)stage[f * fs + 2 * r + 1] << 32) | stage[f * fs + 2 * r], out + e);
-    }
+    if (live && present) __builtin_nontemporal_store(mask, present + i);
 }
 
 }  // namespace
@@ -197,7 +209,7 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
         return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t grid = (b->n + kFieldBlock - 1) / kFieldBlock;
-    const size_t lds = (size_t)kFieldBlock * (2 * n_req + 1) * 4;
+    const size_t lds = (size_t)kFieldBlock * (2 * kReqGroup + 1) * 4;
     return launch(fields_kernel, dim3(grid), dim3(kFieldBlock), lds, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
                   layers_dev, rq, n_req, values_dev, present_dev);
