@@ -775,6 +775,14 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
 // taking the next untaken frame when its walk ends (82.9 -> 68.7 us on the capture
 // mix vs four fixed frames per lane, profiles/r02_fwd/ablate_layers_c9.log)
 constexpr int kLayFrames = 4;
+// A lane stores its 64-B record as four 16-B stores when its walk ends, so every store
+// instruction writes 16 B into each of up to 64 different records: with the default
+// policy L2 merges a record's four pieces into one line write, non-temporal stores do not
+// (config 2 walk 60.3 -> 42.2 us, config 5 337.6 -> 312.6 us, capture mix 59.1 -> 58.3 us,
+// same process, profiles/r02_ab_recnt).
+#ifndef RPKT_LAY_REC_NT
+#define RPKT_LAY_REC_NT 0        // 1: record stores non-temporal
+#endif
 #ifndef RPKT_LAY_BLOCK_POOL
 #define RPKT_LAY_BLOCK_POOL 1    // 0: one pool per wave
 #endif
@@ -913,9 +921,14 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             if (stop) {
                 u32x4* dst = reinterpret_cast<u32x4*>(out + i);
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k) {
+#if RPKT_LAY_REC_NT
                     __builtin_nontemporal_store(u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]},
                                                 &dst[k]);
+#else
+                    dst[k] = u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+#endif
+                }
                 Frame f = fr[0];
                 if constexpr (DYN) {
                     const uint32_t k = kbase + rank;
