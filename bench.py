@@ -246,7 +246,8 @@ def pmc_traffic_tx(leg):
         return None, None
     unit = {"build": "tx", "forward": "tx", "opts": "walks", "optsc": "walks", "layers": "walks",
             "fields": "fields"}[leg.rstrip("0123456789")]
-    if leg not in t["legs"] or not same_unit(t.get("engine_build"), unit):
+    if leg not in t["legs"] or not same_unit(t["legs"][leg].get("engine_build", t.get("engine_build")),
+                                             unit):
         return None, None
     return int(t["legs"][leg]["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
 

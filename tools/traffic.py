@@ -63,6 +63,18 @@ TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "opt
            "layers9": "layers_kernel", "fields9": "fields_kernel"}
 
 
+LEG_UNIT = {"build": "tx", "forward": "tx", "opts": "walks", "optsc": "walks", "layers": "walks",
+            "fields": "fields"}
+
+
+def unit_hash(build, unit):
+    """The `<unit>=<hash>` token of an engine build string (rpkt_gpu_build_info)."""
+    for tok in (build or "").replace(";", " ").split():
+        if tok.startswith(unit + "="):
+            return tok
+    return None
+
+
 MODE_KERNEL = {"build": "build_kernel", "forward": "forward_kernel", "opts": "options_kernel",
                "optsc": "options_kernel",
                "layers": "layers_kernel", "fields": "fields_kernel"}
@@ -82,11 +94,22 @@ def main_tx(prof, out, only=None):
             if line.startswith("{"):
                 build = json.loads(line).get("engine_build")
     legs = {}
-    if only:
+    old = {}
+    if os.path.exists(out):
         with open(out) as fh:
             old = json.load(fh)
-        assert old["engine_build"] == build, (old["engine_build"], build)
+    if only:
+        assert old.get("engine_build") == build, (old.get("engine_build"), build)
         legs = old["legs"]
+    else:
+        # the single-leg profiles (build3, optsc5) stay while their kernel unit's source
+        # is unchanged; each leg carries the build it was measured on
+        for leg, v in old.get("legs", {}).items():
+            if leg in TX_LEGS:
+                continue
+            unit = LEG_UNIT[leg.rstrip("0123456789")]
+            if unit_hash(v.get("engine_build", old.get("engine_build")), unit) == unit_hash(build, unit):
+                legs[leg] = dict(v, engine_build=v.get("engine_build", old.get("engine_build")))
     todo = TX_LEGS.items() if not only else \
         [(only, next(k for m, k in MODE_KERNEL.items() if only.startswith(m)))]
     for leg, kname in todo:
@@ -95,11 +118,13 @@ def main_tx(prof, out, only=None):
             continue
         legs[leg] = {"kernel": kname, "fetch_size_kib": f, "write_size_kib": w,
                      "hbm_read_bytes_corrected": f * 1024 * 2, "hbm_write_bytes": w * 1024,
-                     "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024}
+                     "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024, "engine_build": build}
     res = {"engine_build": build, "legs": legs,
            "kernel_stats": rows(os.path.join(prof, "trace_kernel_stats.csv"))}
-    if only:                                   # keep the other single-leg profiles' stats
-        res.update({k: v for k, v in old.items() if k.startswith("kernel_stats")})
+    # keep the stats of the single-leg profiles whose legs were kept
+    res.update({k: v for k, v in old.items()
+                if k.startswith("kernel_stats_") and k[len("kernel_stats_"):] in legs})
+    if only:
         res["kernel_stats_" + only] = rows(os.path.join(prof, "trace_kernel_stats.csv"))
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
