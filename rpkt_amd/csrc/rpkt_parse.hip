@@ -597,7 +597,13 @@ void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_byte
 // slice) and a u32 {ip_bad | l4_bad << 16}, writes them once to its slab, and a
 // second kernel sums the slabs in a fixed order (bitwise reproducible counters).
 // Slab layout: u64[rows] then u32[rows] (3 * rows dwords).
-constexpr int kFlowThreads = 512;
+// 16 waves per block, one block per CU (its LDS histogram): 1M events 14.8 -> 12.6 us
+// against 8 waves, 8M events 25.2 vs 25.5 us; 4 waves slower at both sizes
+// (profiles/r02_ab_flowthreads)
+#ifndef RPKT_FLOW_THREADS
+#define RPKT_FLOW_THREADS 1024
+#endif
+constexpr int kFlowThreads = RPKT_FLOW_THREADS;
 constexpr uint32_t kFlowLdsMax = 8192;      // buckets (+1 unparsed row) privatised in LDS
 constexpr uint32_t kFlowMaxPerBlock = 32768;
 constexpr uint32_t kFlowMinBlocks = 256;
