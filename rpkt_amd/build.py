@@ -25,7 +25,13 @@ GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
 GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 # units compiled a second time with other defines (same source: same unit hash)
-SECOND_COMPILES = [("rpkt_tx.hip", "rpkt_tx_w64.o", ["-DRPKT_WIN=64", "-DRPKT_TX_W64"])]
+SECOND_COMPILES = [("rpkt_tx.hip", "rpkt_tx_w64.o", ["-DRPKT_WIN=64", "-DRPKT_TX_W64"]),
+                   # only the compact parse of short strided frames: the unit's other
+                   # kernels are not used by this compile
+                   ("rpkt_parse.hip", "rpkt_parse_w64.o", ["-DRPKT_WIN=64", "-DRPKT_PARSE_W64",
+                                                           "-Wno-unused-function",
+                                                           "-Wno-unused-const-variable",
+                                                           "-Wno-unneeded-internal-declaration"])]
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
 HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 

@@ -793,7 +793,39 @@ __global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
 
 }  // namespace
 
+// This unit compiles twice: as is (128-B windows) and with RPKT_PARSE_W64 (RPKT_WIN 64,
+// rpkt_amd/build.py), whose only entry point is the hidden
+// rpkt_gpu_parse_batch_compact_w64 the first compile hands strided batches of short
+// frames to: every frame lies inside its 64-B window (parse_w64_fits), so the headers
+// and the L4 bytes are all in LDS, a wave's LDS drops from 9.7 to 5.6 KB, and with the
+// 16-B records kept in registers the VGPRs, not the LDS, set the waves per SIMD.
+#ifndef RPKT_PARSE_W64_ON
+#define RPKT_PARSE_W64_ON 1
+#endif
+
 extern "C" {
+
+#ifdef RPKT_PARSE_W64
+__attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
+    const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
+    uint32_t n_buckets, void* stream) {
+    const uint32_t flen = b->frame_len ? b->frame_len : b->stride;
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+#else
+int rpkt_gpu_parse_batch_compact_w64(const rpkt_batch_t*, uint32_t, rpkt_rec16_t*,
+                                     rpkt_flow_ev_t*, uint32_t, void*);
+
+// every frame of a strided batch inside a 64-B window from its 16-B boundary
+static bool parse_w64_fits(const rpkt_batch_t* b, uint32_t flen) {
+    if (b->offsets_dev || b->stride == 0 || flen == 0) return false;
+    return flen + ((b->stride & 15u) ? 15u : 0u) <= 64u;
+}
 
 uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_t dp,
                         uint8_t proto) {
@@ -848,6 +880,8 @@ int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec
         if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
     }
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    if (RPKT_PARSE_W64_ON && parse_w64_fits(b, flen))
+        return rpkt_gpu_parse_batch_compact_w64(b, flags, recs_dev, flow_ev_dev, n_buckets, stream);
     const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
@@ -1001,5 +1035,7 @@ int rpkt_gpu_checksum_chains(const uint8_t* buf, uint64_t buf_bytes, const uint3
     return launch(chain_fold_kernel, dim3((n_chains + 255) / 256), dim3(256), 0, st,
                   (const uint32_t*)workspace, chain_first, n_chains, n_segs, out);
 }
+
+#endif  // RPKT_PARSE_W64
 
 }  // extern "C"

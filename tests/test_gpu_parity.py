@@ -370,3 +370,9 @@ def test_short_strided_frames(torch, stride, flen):
         o = oracle_records(hb, flags)
         assert_same(gpu_records(hb, flags), o)
         assert_same16(gpu_records16(hb, flags), project16(o, flags))
+    # compact records with flow events (frames inside a 64-B window take the 64-B-window
+    # compile of the compact parse)
+    g, gev = gpu_records16(hb, 3 | F_FLOW_EV, 4096)
+    o, oev = oracle_records(hb, 3, 4096, flow=True)
+    assert_same16(g, project16(o, 3))
+    assert np.array_equal(gev, oev)

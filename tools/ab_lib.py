@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|layers9|forward2|build2|build3|parse2|parse3]
+Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3]
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -101,6 +101,14 @@ def main():
             out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
             flags = 1 if cfg == 2 else 3
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
+                ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
+        elif mode == "parsec":                      # compact records
+            L.rpkt_gpu_parse_batch_compact.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p,
+                                                       ctypes.c_void_p, ctypes.c_uint32,
+                                                       ctypes.c_void_p]
+            out = torch.zeros(hb.n * 16, dtype=torch.uint8, device="cuda")
+            flags = 1 if cfg == 2 else 3
+            call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch_compact(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
         elif mode == "fields":                      # bench.py's 16 getters over the walk
             import bench
