@@ -106,6 +106,9 @@ __device__ __noinline__ Bytes9 load9_bytes(__amdgpu_buffer_rsrc_t rs, uint32_t a
 #define RPKT_FIELDS_GROUP 16
 #endif
 constexpr uint32_t kReqGroup = RPKT_FIELDS_GROUP;
+#ifndef RPKT_FIELDS_SAMELAYER
+#define RPKT_FIELDS_SAMELAYER 1  // requests on the layer of the one before skip the search
+#endif
 
 // One lane per frame: its layer record once, then the requests in groups of sixteen whose
 // 48 dword loads are issued before any is used (the request list is wave-uniform,
@@ -118,7 +121,7 @@ constexpr uint32_t kReqGroup = RPKT_FIELDS_GROUP;
 __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
     const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len, uint32_t n,
-    const rpkt_layers_t* __restrict__ layers, FieldReqs reqs, uint32_t n_req,
+    const rpkt_layers_t* __restrict__ layers, FieldReqs reqs, uint32_t n_req, uint32_t same_prev,
     uint64_t* __restrict__ values, uint32_t* __restrict__ present) {
     extern __shared__ uint32_t stage[];                  // kFieldBlock * (2 kReqGroup + 1)
     const uint32_t base = blockIdx.x * kFieldBlock, t = threadIdx.x, i = base + t;
@@ -131,6 +134,10 @@ __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
     uint64_t* const out = values + (uint64_t)base * n_req;
     uint32_t mask = 0;
+    // the layer of the last request searched: a request naming the same (protocol, nth)
+    // as the one before it (bit r of same_prev, wave-uniform) reuses it
+    uint32_t cur_loff = 0;
+    bool cur_found = false;
     // a group of requests at a time: loads, values into the LDS stage, then the group's
     // values of the block's frames stored as rows of g consecutive u64 per frame (the
     // stage holds one group, so the block's LDS does not limit the waves per CU)
@@ -141,9 +148,13 @@ __global__ __launch_bounds__(kFieldBlock) void fields_kernel(
             for (uint32_t j = 0; j < kReqGroup; ++j) {
                 const rpkt_field_req_t q = reqs.r[r0 + j];
                 const uint32_t eb = ((uint32_t)q.bit_off + q.bits - 1) >> 3;
-                uint32_t loff;
-                ok[j] = find_layer(L, q.proto, q.nth, loff) & (loff + eb < fr.len);
-                a[j] = ok[j] ? fr.off + loff + (q.bit_off >> 3) : 0u;
+#if RPKT_FIELDS_SAMELAYER
+                if (!((same_prev >> (r0 + j)) & 1u)) cur_found = find_layer(L, q.proto, q.nth, cur_loff);
+#else
+                cur_found = find_layer(L, q.proto, q.nth, cur_loff);
+#endif
+                ok[j] = cur_found & (cur_loff + eb < fr.len);
+                a[j] = ok[j] ? fr.off + cur_loff + (q.bit_off >> 3) : 0u;
                 const uint32_t a4 = a[j] & ~3u;
                 d[j][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)a4, 0, 0);
                 d[j][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a4 + 4u), 0, 0);
@@ -192,6 +203,8 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
     if (!b || !layers_dev || !reqs || !values_dev) return RPKT_E_INVAL;
     if (n_req == 0 || n_req > RPKT_MAX_FIELD_REQS) return RPKT_E_INVAL;
     FieldReqs rq = {};
+    uint32_t same_prev = 0;                                 // bit r: request r names the
+                                                            // layer request r - 1 names
     for (uint32_t k = 0; k < RPKT_MAX_FIELD_REQS; ++k)      // padding: matches no layer
         rq.r[k] = rpkt_field_req_t{0xff, 0, 8, 0, 0, 0};
     for (uint32_t k = 0; k < n_req; ++k) {
@@ -199,7 +212,9 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
         if (t.bits == 0 || t.bits > 64 || t.proto >= RPKT_N_PROTOCOLS) return RPKT_E_INVAL;
         if ((uint32_t)t.bit_off + t.bits > 65535u * 8u) return RPKT_E_INVAL;
         rq.r[k] = t;
+        if (k && t.proto == reqs[k - 1].proto && t.nth == reqs[k - 1].nth) same_prev |= 1u << k;
     }
+    for (uint32_t k = n_req + 1; k < RPKT_MAX_FIELD_REQS; ++k) same_prev |= 1u << k;   // padding
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
@@ -212,7 +227,7 @@ int rpkt_gpu_fields_batch(const rpkt_batch_t* b, const rpkt_layers_t* layers_dev
     const size_t lds = (size_t)kFieldBlock * (2 * kReqGroup + 1) * 4;
     return launch(fields_kernel, dim3(grid), dim3(kFieldBlock), lds, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
-                  layers_dev, rq, n_req, values_dev, present_dev);
+                  layers_dev, rq, n_req, same_prev, values_dev, present_dev);
 }
 
 }  // extern "C"
