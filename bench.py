@@ -92,6 +92,11 @@ def sum_over_ranks(x, world):
     return float(t.item())
 
 
+def agree_all(ok, world):
+    """True on every rank iff ok on every rank."""
+    return ok if world == 1 else rdist.agree(ok)
+
+
 def usable_cpus():
     """Host threads this process may run on: the affinity mask, capped by a cgroup v2
     CPU quota when one is set (a GPU box grants a share of a larger machine)."""
@@ -154,7 +159,7 @@ def algorithmic_bytes(hb, flow=False, rec_bytes=REC_BYTES):
 
 
 def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3,
-               compact=False):
+               compact=False, opts=None):
     """Time `steps` launches (rotating over dbs).  Returns wall seconds (max over
     ranks) and the mean per-launch device time from two HIP events recorded on the
     launch stream around the back-to-back launches."""
@@ -169,6 +174,9 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
                                n_buckets=nb, stream=stream)
             engine.flow_count(flow["ev"][k % R], db.n, nb, counters=flow["counters"],
                               workspace=flow["ws"], stream=stream)
+        elif opts is not None:                         # parse + option walks, one pass
+            engine.parse_options_batch(db, flags, recs=rc, opts=opts[k % R], stream=stream,
+                                       compact=compact)
         elif isinstance(db, engine.DeviceChains):
             engine.parse_chains(db, flags, recs=rc, stream=stream)
         elif compact:
@@ -205,11 +213,12 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
     return wall, kern_ms, warm_launches
 
 
-def pmc_traffic(cfg, compact=False):
-    """Per-launch HBM traffic of parse_kernel for this config (and record size) from the
-    rocprofv3 PMC summary committed under profiles/ (tools/traffic.py), when it was
-    measured on this exact engine build; else None."""
-    path = os.path.join(ROOT, "profiles", "traffic_c%d%s.json" % (cfg, "_compact" if compact else ""))
+def pmc_traffic(cfg, compact=False, opts=False):
+    """Per-launch HBM traffic of parse_kernel for this config (and record size, and the
+    fused option walks) from the rocprofv3 PMC summary committed under profiles/
+    (tools/traffic.py), when it was measured on this exact engine build; else None."""
+    path = os.path.join(ROOT, "profiles", "traffic_c%d%s%s.json" % (
+        cfg, "_opts" if opts else "", "_compact" if compact else ""))
     try:
         with open(path) as fh:
             t = json.load(fh)
@@ -396,15 +405,27 @@ def layout_name(hb):
     return ("stride%d" % hb.stride) if hb.stride else "packed+u32 offsets"
 
 
-def run_config(cfg, args, rank, world, cpu=False, compact=False):
+def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, strong=False):
     """One parse leg: config `cfg`'s batches resident, K timed launches.  compact: the
-    16-byte record entry point (rpkt_gpu_parse_batch_compact) instead of the 80-byte one."""
+    16-byte record entry point (rpkt_gpu_parse_batch_compact) instead of the 80-byte one.
+    opts: the fused parse + option walks (rpkt_gpu_parse_options_batch[_compact]), 64 B
+    more written per frame.  strong: configs 2/3 as one batch split over the ranks
+    (rdist.shard_range), each rank rotating over enough distinct batches that its shards
+    outgrow the 256 MiB Infinity Cache twice over."""
     flags = gen.FLAGS[cfg]
     flow = None
     if cfg == 4:                                   # strong scaling: shard one 8M batch
         n_total = args.frames or gen.DEFAULT_N[4]
         lo, hi = rdist.shard_range(n_total, rank, world)
         hbs = [gen.make_batch(4, hi - lo, first=lo)]
+        scaling = "strong"
+    elif strong:                                   # strong scaling: shard one batch
+        n_total = args.frames or gen.DEFAULT_N[cfg]
+        lo, hi = rdist.shard_range(n_total, rank, world)
+        shard_bytes = max(1, (hi - lo) * gen.STRIDED.get(cfg, 1024))
+        R = max(8 if cfg == 2 else 1, -(-(512 << 20) // shard_bytes))
+        hbs = [gen.make_batch(cfg, hi - lo, seed=gen.DEFAULT_SEED[cfg] + 104729 * r, first=lo)
+               for r in range(R)]
         scaling = "strong"
     elif cfg in gen.CHAINED:                       # weak scaling: chains per rank
         n = args.frames or gen.DEFAULT_N[cfg]
@@ -420,6 +441,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
            engine.DeviceBatch.from_host(hb) for hb in hbs]
     rec_bytes = REC16_BYTES if compact else REC_BYTES
     recs = [torch.empty(hb.n * rec_bytes, dtype=torch.uint8, device="cuda") for hb in hbs]
+    obufs = [torch.empty(hb.n * 64, dtype=torch.uint8, device="cuda") for hb in hbs] if opts else None
     if cfg == 4:
         nb = 8192
         flow = {"n_buckets": nb,
@@ -430,19 +452,24 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
     log(rank, "config %d: %d frames/rank x %d batches resident, flags=%d" % (
         cfg, hbs[0].n, len(hbs), flags))
     wall, kern_ms, warm = time_parse(dbs, recs, flags, args.steps, args.warmup, world, flow,
-                                     args.min_warmup_s, compact)
+                                     args.min_warmup_s, compact, obufs)
 
     frames_step = sum(hb.n for hb in hbs) / len(hbs)
     bytes_step = sum(int(hb.lens().sum()) for hb in hbs) / len(hbs)
-    alg_step = sum(algorithmic_bytes(hb, flow is not None, rec_bytes) for hb in hbs) / len(hbs)
-    mpps = frames_step * world * args.steps / wall / 1e6
-    gbps = bytes_step * world * args.steps / wall / 1e9
+    alg_step = sum(algorithmic_bytes(hb, flow is not None, rec_bytes + (64 if opts else 0))
+                   for hb in hbs) / len(hbs)
+    # whole-job frames per step: every rank's shard (they differ by at most one frame)
+    frames_job = sum_over_ranks(frames_step, world) if scaling == "strong" else frames_step * world
+    bytes_job = sum_over_ranks(bytes_step, world) if scaling == "strong" else bytes_step * world
+    mpps = frames_job * args.steps / wall / 1e6
+    gbps = bytes_job * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic(cfg, compact)
+    traffic, tsrc = pmc_traffic(cfg, compact, opts)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
         "warmup_launches": warm,
         "kernel_ms": kern_ms, "scaling": scaling, "frames_per_rank": int(frames_step),
+        "frames_per_step": int(frames_job), "batches_rotated": len(hbs),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": tsrc,
@@ -453,25 +480,41 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False):
     if compact:
         out["what"] = ("rpkt_gpu_parse_batch_compact: the same parse + sums, 16-B records "
                        "(status, offsets, sums, verdicts)")
+    if opts:
+        out["what"] = ("rpkt_gpu_parse_options_batch%s: the parse + sums and both option walks "
+                       "(Ipv4OptionsIter, TcpOptionsIter) in one pass, 64-B rpkt_opts_t per frame"
+                       % ("_compact" if compact else ""))
     if cfg == 4:
         torch.cuda.synchronize()
         barrier(world)
+        # the per-rank counters, kept to check the product reduce against torch's own
+        local = flow["counters"].clone() if world > 1 else None
+        torch.cuda.synchronize()
+        barrier(world)
         t0 = time.perf_counter()
-        try:
-            via = rdist.reduce_counters(flow["counters"], nb)    # rpkt_gpu_flow_reduce (RCCL)
-        except engine.RpktError as e:                  # nothing was enqueued: same sum via torch
-            dist.all_reduce(flow["counters"], op=dist.ReduceOp.SUM)
-            via = "torch.distributed all_reduce (C ABI reduce refused: %s)" % e
+        # rpkt_gpu_flow_reduce (RCCL, C ABI) when every rank can call it, else torch's
+        # all-reduce on every rank; a failure after the group chose the C ABI raises
+        rdist.reduce_counters(flow["counters"], n_buckets=nb)
         torch.cuda.synchronize()
         red = time.perf_counter() - t0
         c = rdist.counters_as_u64(flow["counters"])
         out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
-        out["flow_reduce_via"] = via
+        out["flow_reduce_via"] = rdist.last_reduce_path
+        if rdist.last_reduce_error:
+            out["flow_reduce_error"] = "C ABI reduce not taken: %s" % rdist.last_reduce_error
+        if local is not None:                        # every word vs torch.distributed's sum
+            rdist.reduce_counters(local, via="torch")
+            same = torch.equal(local, flow["counters"])
+            out["flow_reduce_verified"] = bool(agree_all(same, world))
+            if not out["flow_reduce_verified"]:
+                out["flow_reduce_error"] = ("reduced counters differ from torch.distributed's "
+                                            "all_reduce of the same per-rank counters")
         out["flow_pkts_total"] = int(c[:, 0].sum())
         # every launch (warmup included) added its shard's frames to the counters
         out["flow_pkts_expected"] = int(sum_over_ranks(hbs[0].n * (args.steps + warm), world))
     # the records of batch 0 are read back before the copy references overwrite them
-    g = as_records(recs[0].cpu().numpy()) if cpu and rank == 0 and not compact else None
+    g = as_records(recs[0].cpu().numpy()) if cpu and rank == 0 and not compact and not opts \
+        else None
     if cfg == 2 and not compact:
         out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
     if g is not None:
@@ -492,7 +535,7 @@ def copy_ceiling(dbs, recs, steps):
     own bytes (the 8 rotated 64 MiB frame buffers read, 80 MiB of records written:
     rpkt_gpu_debug_variant 13, tools/ablate.py's v13); (2) hipMemcpyAsync device to
     device of 1 GiB (torch copy_), read + written bytes counted."""
-    L = engine.lib()
+    L = engine.ablate_lib()               # the streaming references: development library
     L.rpkt_gpu_debug_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     L.rpkt_gpu_debug_variant.restype = ctypes.c_int
@@ -698,8 +741,16 @@ def main():
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
     ap.add_argument("--record", default="full", choices=["full", "compact"],
                     help="record size of the main leg (profiling the compact kernel alone)")
+    ap.add_argument("--main-opts", action="store_true",
+                    help="main leg as the fused parse + option walks (profiling it alone)")
     ap.add_argument("--compact", default="2,3",
                     help="configs also timed with 16-B compact records (extra.config<N>_compact)")
+    ap.add_argument("--strong", default="2,3",
+                    help="configs also timed as one batch split over the ranks "
+                         "(extra.config<N>_strong)")
+    ap.add_argument("--opts", default="5",
+                    help="configs also timed as the fused parse + option walks "
+                         "(extra.config<N>_opts, extra.config<N>_opts_compact)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -739,8 +790,8 @@ def main():
     if not args.cpu_threads:
         args.cpu_threads = usable_cpus()
 
-    main_res = run_config(args.config, args, rank, world, cpu=want_cpu,
-                          compact=args.record == "compact")
+    main_res = run_config(args.config, args, rank, world, cpu=want_cpu and not args.main_opts,
+                          compact=args.record == "compact", opts=args.main_opts)
     extra = {}
     for c in [int(x) for x in args.also.split(",") if x.strip()]:
         if c != args.config:
@@ -749,6 +800,12 @@ def main():
         extra["tx_" + leg] = run_tx(cfg, mode, args, rank, world)
     for c in [int(x) for x in args.compact.split(",") if x.strip()]:
         extra["config%d_compact" % c] = run_config(c, args, rank, world, compact=True)
+    for c in [int(x) for x in args.strong.split(",") if x.strip()]:
+        extra["config%d_strong" % c] = run_config(c, args, rank, world, strong=True)
+    for c in [int(x) for x in args.opts.split(",") if x.strip()]:
+        extra["config%d_opts" % c] = run_config(c, args, rank, world, opts=True)
+        extra["config%d_opts_compact" % c] = run_config(c, args, rank, world, compact=True,
+                                                        opts=True)
     if want_cpu and not args.no_config1:
         extra["config1"] = run_config1(args)
 
@@ -782,14 +839,22 @@ def main():
             "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                           for kk, vv in v.items()} for k, v in extra.items()},
         }
-        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_pkts_total", "flow_pkts_expected",
-                  "copy_ceiling"):
+        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified", "flow_reduce_error",
+                  "flow_pkts_total", "flow_pkts_expected", "copy_ceiling"):
             if k in main_res:
                 line[k] = main_res[k]
         print(json.dumps(line), flush=True)
+    # a counter sum that is wrong (not merely taken by the fallback path) fails the run
+    bad_counters = any(r.get("flow_reduce_verified") is False or
+                       r.get("flow_pkts_total", 0) != r.get("flow_pkts_expected", 0)
+                       for r in [main_res] + list(extra.values()))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if bad_counters:
+        print("[bench] error: flow counters wrong after the reduce (see flow_reduce_error)",
+              file=sys.stderr)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -392,6 +392,22 @@ int rpkt_gpu_options_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev
 int rpkt_gpu_options_batch_compact(const rpkt_batch_t* batch, const rpkt_rec16_t* recs_dev,
                                    rpkt_opts_t* opts_dev, void* stream);
 
+/* Parse + verify and the option walks in one pass: rpkt_gpu_parse_batch's records (and
+ * flow events) plus, per frame, the rpkt_opts_t that rpkt_gpu_options_batch would
+ * produce from those records -- the walks run on the header bytes the parse has just
+ * read, as rpkt's iterators walk the var_header_slice() of the views the parse returned
+ * (ipv4/generated.rs:57-60, 1625-1722; tcp/generated.rs:1387-1484), so the option bytes
+ * are not fetched a second time.  Outputs are byte-identical to the two separate calls.
+ * opts_dev n * 64 B, 16-byte aligned. */
+int rpkt_gpu_parse_options_batch(const rpkt_batch_t* batch, uint32_t flags,
+                                 rpkt_rec_t* recs_dev, rpkt_opts_t* opts_dev,
+                                 rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
+/* The same with compact records (rpkt_gpu_parse_batch_compact's rpkt_rec16_t). */
+int rpkt_gpu_parse_options_batch_compact(const rpkt_batch_t* batch, uint32_t flags,
+                                         rpkt_rec16_t* recs_dev, rpkt_opts_t* opts_dev,
+                                         rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets,
+                                         void* stream);
+
 /* ---- Protocol layer walk ---------------------------------------------------------- */
 
 /* The protocol stack of each frame, walked with the header views of every protocol

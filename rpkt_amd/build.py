@@ -1,7 +1,7 @@
 """Build the native libraries in-tree (they travel to the GPU box with the repo).
 
-  rpkt_amd/_build/librpkt_gpu.so   HIP engine for gfx950 + C ABI (include/rpkt_gpu.h),
-                                   linked to RCCL for rpkt_gpu_flow_reduce
+  rpkt_amd/_build/librpkt_gpu.so   HIP engine for gfx950 + C ABI (include/rpkt_gpu.h);
+                                   RCCL (rpkt_gpu_flow_reduce) is resolved at first use
   rpkt_amd/_build/librpkt_gen.so   host C++ synthetic frame generator
 
 hipcc cross-compiles gfx950 without a GPU.  Rebuilds only when a source is newer.
@@ -17,12 +17,16 @@ ARCH = os.environ.get("RPKT_OFFLOAD_ARCH", "gfx950")
 ROCM_LIB = "/opt/rocm/lib"
 
 GPU_LIB = os.path.join(OUT, "librpkt_gpu.so")
+# the same units with -DRPKT_ABLATE: the product entry points plus the development hooks
+# (kernel ablation variants, streaming references) that tools/ and bench.py's
+# copy_ceiling call; the product library exports exactly include/rpkt_gpu.h
+ABLATE_LIB = os.path.join(OUT, "librpkt_gpu_ablate.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
 # the engine: one translation unit per kernel family, shared device code in rpkt_common.h
 GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
            ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_abi.hip",
             "rpkt_coll.hip")]
-GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"),
+GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"), os.path.join(HERE, "csrc", "rpkt_opts.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 # units compiled a second time with other defines (same source: same unit hash)
 SECOND_COMPILES = [("rpkt_tx.hip", "rpkt_tx_w64.o", ["-DRPKT_WIN=64", "-DRPKT_TX_W64"]),
@@ -67,22 +71,32 @@ def unit_hashes():
 
 
 def build_gpu(force=False, extra=()):
-    """Compile the units in parallel (hipcc -c, gfx950), then link the shared library."""
+    """Compile the units in parallel (hipcc -c, gfx950), then link the product library and
+    the development library (-DRPKT_ABLATE)."""
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OUT, exist_ok=True)
-    if not (force or _stale(GPU_LIB, GPU_SRC + GPU_DEPS + HDR)):
+    deps = GPU_SRC + GPU_DEPS + HDR
+    if not (force or _stale(GPU_LIB, deps) or _stale(ABLATE_LIB, deps)):
         return GPU_LIB
     flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
              '-DRPKT_SRC_HASH="%s"' % source_hash(), '-DRPKT_UNIT_HASHES="%s"' % unit_hashes()] + \
         list(extra)
-    jobs = [(f, os.path.join(OUT, os.path.basename(f).replace(".hip", ".o")), []) for f in GPU_SRC]
-    jobs += [(os.path.join(HERE, "csrc", src), os.path.join(OUT, obj), d) for src, obj, d in SECOND_COMPILES]
-    objs = [o for _, o, _ in jobs]
-    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+    units = [(f, os.path.basename(f)[:-4], []) for f in GPU_SRC]
+    units += [(os.path.join(HERE, "csrc", src), obj[:-2], d) for src, obj, d in SECOND_COMPILES]
+    libs = {GPU_LIB: [], ABLATE_LIB: []}
+    jobs = []
+    for src, stem, d in units:
+        for lib, sfx, dd in ((GPU_LIB, "", []), (ABLATE_LIB, "_ablate", ["-DRPKT_ABLATE"])):
+            obj = os.path.join(OUT, stem + sfx + ".o")
+            jobs.append((src, obj, d + dd))
+            libs[lib].append(obj)
+    with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
         list(ex.map(lambda j: subprocess.check_call(flags + j[2] + ["-c", "-o", j[1], j[0]]), jobs))
-    # librccl.so.1 by soname: under torch it resolves to the RCCL torch already loaded
-    subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", GPU_LIB] + objs +
-                          ["-L" + ROCM_LIB, "-lrccl"])
+    # RCCL is not linked: rpkt_coll.hip resolves it on first use (the copy already in the
+    # process first, so under torch the communicator and the library match)
+    for lib, objs in libs.items():
+        subprocess.check_call([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] +
+                              objs + ["-ldl"])
     return GPU_LIB
 
 

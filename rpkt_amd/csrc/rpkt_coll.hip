@@ -7,15 +7,45 @@
 // the per-queue counters a DPDK receive loop keeps per thread and adds up at the
 // end (rpkt-dpdk/examples/loopback_tx.rs:176-181, rss_rx.rs:54-113).
 //
-// The library links librccl.so.1 by soname: under PyTorch the communicator comes
-// from ProcessGroupNCCL and the soname resolves to the RCCL torch already loaded;
-// a C/C++/Rust host gets /opt/rocm's RCCL and its own ncclCommInit*.
+// RCCL is resolved when the collective is first used, not at load time, so a parse-only
+// host (C, C++, Rust) loads the engine without RCCL installed.  The communicator must
+// belong to the RCCL copy in the process: one already loaded (PyTorch's, whose
+// ProcessGroupNCCL made the communicator; found with RTLD_NOLOAD) is preferred over
+// loading librccl.so.1 afresh (/opt/rocm's, for hosts that call ncclCommInit*
+// themselves).  Without RCCL the calls return RPKT_E_COLL.
 #include "rpkt_common.h"
 
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <mutex>
+#include <rccl/rccl.h>        // types and enums only: every function goes through Rccl
 
 namespace {
 thread_local int g_last_coll_error = 0;
+
+struct Rccl {
+    decltype(&ncclGetVersion) get_version = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    bool ok = false;
+};
+
+const Rccl& rccl() {
+    static Rccl R;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        R.get_version = (decltype(R.get_version))dlsym(h, "ncclGetVersion");
+        R.comm_count = (decltype(R.comm_count))dlsym(h, "ncclCommCount");
+        R.all_reduce = (decltype(R.all_reduce))dlsym(h, "ncclAllReduce");
+        R.reduce = (decltype(R.reduce))dlsym(h, "ncclReduce");
+        R.ok = R.get_version && R.comm_count && R.all_reduce && R.reduce;
+    });
+    return R;
+}
 }  // namespace
 
 extern "C" {
@@ -23,8 +53,9 @@ extern "C" {
 int rpkt_gpu_last_coll_error(void) { return g_last_coll_error; }
 
 int rpkt_gpu_coll_version(void) {
+    const Rccl& R = rccl();
     int v = 0;
-    return ncclGetVersion(&v) == ncclSuccess ? v : -1;
+    return R.ok && R.get_version(&v) == ncclSuccess ? v : -1;
 }
 
 int rpkt_gpu_flow_reduce(uint64_t* counters_dev, uint32_t n_buckets, int root, void* nccl_comm,
@@ -33,16 +64,21 @@ int rpkt_gpu_flow_reduce(uint64_t* counters_dev, uint32_t n_buckets, int root, v
         root < -1)
         return RPKT_E_INVAL;
     if (((uintptr_t)counters_dev & 7u) != 0) return RPKT_E_ALIGN;
+    const Rccl& R = rccl();
+    if (!R.ok) {
+        g_last_coll_error = (int)ncclSystemError;           // no RCCL in this process
+        return RPKT_E_COLL;
+    }
     ncclComm_t comm = (ncclComm_t)nccl_comm;
     int nranks = 0;
-    ncclResult_t r = ncclCommCount(comm, &nranks);
+    ncclResult_t r = R.comm_count(comm, &nranks);
     if (r == ncclSuccess && root >= nranks) return RPKT_E_INVAL;
     const size_t count = ((size_t)n_buckets + 1) * 4;
     hipStream_t s = (hipStream_t)stream;
     if (r == ncclSuccess)
-        r = root < 0 ? ncclAllReduce(counters_dev, counters_dev, count, ncclUint64, ncclSum, comm, s)
-                     : ncclReduce(counters_dev, counters_dev, count, ncclUint64, ncclSum, root,
-                                  comm, s);
+        r = root < 0 ? R.all_reduce(counters_dev, counters_dev, count, ncclUint64, ncclSum, comm, s)
+                     : R.reduce(counters_dev, counters_dev, count, ncclUint64, ncclSum, root,
+                                comm, s);
     if (r != ncclSuccess) {
         g_last_coll_error = (int)r;
         return RPKT_E_COLL;

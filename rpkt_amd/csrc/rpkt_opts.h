@@ -1,0 +1,406 @@
+// rpkt_opts.h — the IPv4 / TCP option walks (Ipv4OptionsIter over
+// ipv4.var_header_slice(), ipv4/generated.rs:1595-1722; TcpOptionsIter over
+// tcp.var_header_slice(), tcp/generated.rs:1357-1484) as lane-per-frame device code over
+// option bytes held in LDS.  Shared by the standalone walk over a parsed batch
+// (options_kernel, rpkt_walks.hip) and the walk fused into the parse (parse_kernel with
+// OPTS, rpkt_parse.hip), which runs it on the header window the parse already holds.
+// oracle/rpkt_oracle_opts.c restates the same iterators and cites them line by line.
+#pragma once
+#include "rpkt_common.h"
+
+#ifndef RPKT_OPT_PAIRED
+#define RPKT_OPT_PAIRED 1        // 0: both walks of a frame stepped together (walk_options)
+#endif
+
+namespace {
+
+// Option bytes in LDS: frame byte x of this lane at base[x + bias].
+struct OptWin {
+    const uint8_t* base;                       // the lane's slot (4-aligned)
+    uint32_t bias;
+    // frame bytes x..x+3, little-endian: two aligned LDS dwords and a byte align
+    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
+        const uint32_t y = x + bias, a = y & ~3u;
+        return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
+    }
+    __device__ __forceinline__ uint32_t be32(uint32_t x) const { return bswap32(dw(x)); }
+};
+
+// The per-type parse rules of the generated option views, as a table per option type
+// read from LDS in the walk (a per-lane type would make a switch divergent): kind
+// index (2..7; 0: not an option type of this iterator) | fixed << 3 | x << 4, where the
+// option needs n >= x remaining bytes and header_len == x (fixed) or x <= header_len
+// <= n.  Types 0 (EOL) and 1 (NOP), kinds 0 and 1 of both iterators, are length-1
+// options consumed by opt_run.
+__device__ inline uint32_t opt_rule(bool tcp, uint32_t t) {
+    if (tcp) {
+        switch (t) {
+            case 2: return 2u | 8u | 4u << 4;      // Mss
+            case 3: return 3u | 8u | 3u << 4;      // WindowScale
+            case 4: return 4u | 8u | 2u << 4;      // SackPermitted
+            case 5: return 5u | 2u << 4;           // Sack
+            case 8: return 6u | 8u | 10u << 4;     // Timestamp
+            case 34: return 7u | 2u << 4;          // FastOpen
+            default: return 0u;
+        }
+    }
+    switch (t) {
+        case 68: return 2u | 4u << 4;              // Timestamp
+        case 7: return 3u | 3u << 4;               // RecordRoute
+        case 148: return 4u | 8u | 4u << 4;        // RouteAlert
+        case 134: return 5u | 6u << 4;             // CommercialSecurity
+        case 137: return 6u | 8u | 7u << 4;        // StrictSourceRoute
+        case 131: return 7u | 8u | 7u << 4;        // LooseSourceRoute
+        default: return 0u;
+    }
+}
+
+// Both iterators' rule tables (IPv4: [0, 256), TCP: [256, 512)) into the block's LDS;
+// the caller synchronises the block before the walks read them.
+__device__ __forceinline__ void opt_rules_fill(uint8_t* rules) {
+    static_assert(kWave * kWavesPerBlock >= 256, "one fill pass");
+    if (threadIdx.x < 256) {
+        rules[threadIdx.x] = (uint8_t)opt_rule(false, threadIdx.x);
+        rules[256 + threadIdx.x] = (uint8_t)opt_rule(true, threadIdx.x);
+    }
+}
+
+// option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown type
+__device__ __forceinline__ int opt_len(uint32_t rule, uint32_t d0, uint32_t n, int& kind) {
+    const uint32_t hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
+    const uint32_t x = rule >> 4;
+    const bool fixed = (rule & 8u) != 0u;
+    const bool ok = (n >= x) & (fixed ? hl == x : (hl >= x) & (hl <= n));
+    kind = (int)(rule & 7u);
+    return (rule & 7u) == 0u ? -1 : (ok ? (int)(fixed ? x : hl) : 0);
+}
+
+// One step of a TLV walk (state of Ipv4OptionsIter / TcpOptionsIter): the two walks of
+// a frame are independent, so the kernel steps both in one loop and their LDS round
+// trips overlap.
+struct OptWalk {
+    uint32_t lo, nb, pos, cnt, kinds, stop;
+    uint64_t trace;
+    bool on;
+};
+
+// A run of one-byte options of one type (EOL = kind 0, NOP = kind 1 in both iterators:
+// each is an option of length 1 and the walk goes on) is consumed up to four at a
+// time from the dword at the cursor: padding runs are most of a walk's steps.
+__device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
+    const uint32_t t0 = d0 & 0xffu;
+    if (t0 > 1u) return false;
+    const uint32_t x = d0 ^ (t0 ? 0x01010101u : 0u);   // zero bytes: the same type
+    uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+    k = k < w.nb - w.pos ? k : w.nb - w.pos;            // >= 1: byte 0 matches
+    w.kinds |= 1u << t0;
+    if (w.cnt < 16) {
+        const uint32_t nib = (t0 ? 0x2222u : 0x1111u) & ((1u << (4 * k)) - 1u);   // k <= 4
+        w.trace |= (uint64_t)nib << (4 * w.cnt);
+    }
+    w.cnt += k;
+    w.pos += k;
+    w.on = w.pos < w.nb;
+    return true;
+}
+
+// The option slices of a parsed frame (what the walks read from its record): the IPv4
+// slice [l3 + 20, l4) when IPv4 parsed, the TCP slice [l4 + 20, l4 + doff4) when the
+// frame parsed OK as TCP (include/rpkt_gpu.h, rpkt_gpu_options_batch).
+struct OptSlices {
+    bool ip_parsed, tcp;
+    uint32_t ip_lo, ip_hi, t_lo, t_hi;
+    uint32_t need_lo, need_hi;     // frame bytes both walks read: [need_lo, need_hi)
+    bool need;
+};
+
+__device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto, uint32_t l3,
+                                                uint32_t l4, uint32_t doff4) {
+    OptSlices S;
+    S.ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
+    S.tcp = status == RPKT_S_OK && proto == 6u;
+    S.ip_lo = l3 + 20u;
+    S.ip_hi = S.ip_parsed ? l4 : S.ip_lo;
+    S.t_lo = l4 + 20u;
+    S.t_hi = S.tcp ? l4 + doff4 : S.t_lo;
+    S.need_lo = S.ip_hi > S.ip_lo ? S.ip_lo : S.t_lo;
+    S.need_hi = S.t_hi > S.t_lo ? S.t_hi : S.ip_hi;
+    S.need = (S.ip_hi > S.ip_lo) || (S.t_hi > S.t_lo);
+    return S;
+}
+
+// The two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
+// TcpOptionsIter::next, tcp/generated.rs:1400-1484), stepped together, into the 16
+// words of rpkt_opts_t (include/rpkt_gpu.h).  rules: opt_rules_fill's table.
+__device__ __forceinline__ void walk_options(const OptWin& s, const OptSlices& S,
+                                             const uint8_t* rules, uint32_t (&o)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    OptWalk ip{S.ip_lo, S.ip_hi - S.ip_lo, 0, 0, 0, RPKT_OPT_END, 0, S.ip_parsed && S.ip_hi > S.ip_lo};
+    OptWalk tw{S.t_lo, S.t_hi - S.t_lo, 0, 0, 0, RPKT_OPT_END, 0, S.tcp && S.t_hi > S.t_lo};
+    while (ip.on || tw.on) {
+        if (ip.on) {
+            const uint32_t at = ip.lo + ip.pos;
+            const uint32_t d0 = s.dw(at);
+            int kind = 0;
+            const int used = opt_run(ip, d0) ? -2 : opt_len(rules[d0 & 0xffu], d0, ip.nb - ip.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
+                ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                ip.on = false;
+            } else {
+                if (kind == 2) o[9] = (o[9] & 0xff000000u) | (d0 >> 8);
+                if (kind == 3) o[8] = (o[8] & 0xffffu) | ((d0 >> 8) << 16);
+                if (kind == 4) o[8] = (o[8] & 0xffff0000u) | be16_hi(d0);
+                if (kind == 5) o[11] = s.be32(at + 2);
+                if (kind == 6 || kind == 7) {
+                    o[9] = (o[9] & 0x00ffffffu) | ((d0 >> 16) << 24);
+                    o[10] = s.be32(at + 3);
+                }
+                ip.kinds |= 1u << kind;
+                if (ip.cnt < 16) ip.trace |= (uint64_t)(kind + 1) << (4 * ip.cnt);
+                ip.cnt += 1;
+                ip.pos += (uint32_t)used;
+                ip.on = ip.pos < ip.nb;
+            }
+        }
+        if (tw.on) {
+            const uint32_t at = tw.lo + tw.pos;
+            const uint32_t d0 = s.dw(at);
+            int kind = 0;
+            const int used = opt_run(tw, d0) ? -2 : opt_len(rules[256 + (d0 & 0xffu)], d0, tw.nb - tw.pos, kind);
+            if (used == -2) {
+            } else if (used <= 0) {
+                tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                tw.on = false;
+            } else {
+                if (kind == 2) o[1] = (o[1] & 0xffffu) | (be16_hi(d0) << 16);
+                if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (((d0 >> 16) & 0xffu) << 16);
+                if (kind == 5) {
+                    const uint32_t hl = (d0 >> 8) & 0xffu;
+                    o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
+                    o[4] = hl >= 6u ? s.be32(at + 2) : 0u;
+                    o[5] = hl >= 10u ? s.be32(at + 6) : 0u;
+                }
+                if (kind == 6) {
+                    o[2] = s.be32(at + 2);
+                    o[3] = s.be32(at + 6);
+                }
+                if (kind == 7) o[6] = (o[6] & 0xffff0000u) | ((d0 >> 8) & 0xffu);
+                tw.kinds |= 1u << kind;
+                if (tw.cnt < 16) tw.trace |= (uint64_t)(kind + 1) << (4 * tw.cnt);
+                tw.cnt += 1;
+                tw.pos += (uint32_t)used;
+                tw.on = tw.pos < tw.nb;
+            }
+        }
+    }
+    if (S.ip_parsed) {
+        // word 6: tcp_fo_len | tcp_end << 16 | ip_end << 24; word 7: ip_count | ip_stop << 8 | ip_kinds << 16
+        o[6] |= ip.pos << 24;
+        o[7] = ip.cnt | (ip.stop << 8) | (ip.kinds << 16);
+    }
+    if (S.tcp) {
+        // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24; word 1: kinds | mss << 16
+        o[0] = (o[0] & 0xffff0000u) | tw.cnt | (tw.stop << 8);
+        o[1] = (o[1] & 0xffff0000u) | tw.kinds;
+        o[6] = (o[6] & 0xff00ffffu) | (tw.pos << 16);
+    }
+    const uint64_t tcp_trace = tw.trace, ip_trace = ip.trace;
+    o[12] = (uint32_t)tcp_trace;
+    o[13] = (uint32_t)(tcp_trace >> 32);
+    o[14] = (uint32_t)ip_trace;
+    o[15] = (uint32_t)(ip_trace >> 32);
+}
+
+// ---- paired walks: one iterator step per lane per iteration ----
+// walk_options steps a frame's two walks together, so every loop iteration runs both
+// step bodies and a wave runs until its longest walk of either kind ends (config 5: 14.1
+// iterations of two bodies per 64-frame wave, 6.6 walk steps per frame).  Here a lane
+// runs ONE walk at a time with one step body for both iterators (the kind index carries
+// the iterator): first its own frame's TCP walk, then the IPv4 walk of a frame chosen so
+// that long TCP slices meet short IPv4 slices -- lanes ranked by TCP slice length
+// (descending) take the IPv4 walks ranked by slice length (ascending), the k-th with the
+// k-th.  Config 5: 15.3 iterations of one body per wave (a model over its frames), about
+// half the step bodies.  Each lane holds its own frame's TCP words and its partner's
+// IPv4 words of rpkt_opts_t (disjoint words but word 6); both reach their rows through
+// the LDS stage.
+//
+// rank of this lane's key among the wave's keys (0..10), ascending or descending,
+// ties by lane: a permutation of 0..63
+__device__ __forceinline__ uint32_t wave_rank11(uint32_t key, bool descending) {
+    uint32_t rank = 0, base = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 11; ++v) {
+        const uint32_t b = descending ? 10u - v : v;
+        const uint64_t m = __ballot(key == b);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (key == b) rank = base + below;
+        base += (uint32_t)__builtin_popcountll(m);
+    }
+    return rank;
+}
+
+// One iterator's walk over the option bytes at LDS offsets [at, end) of `win`.
+struct OptCur {
+    uint32_t at, end, base, cnt, kinds, stop;
+    uint64_t trace;
+};
+
+// Both slices of this lane's frame as LDS offsets in `win` (slot_off + bias + frame
+// offset), the TCP walk kept, the IPv4 walk handed to the partner lane.  Results go to
+// the stage rows (stride 17 dwords) in `win` once every walk of the wave has ended.
+__device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint32_t slot_bias,
+                                                    const OptSlices& S, const uint8_t* rules,
+                                                    rpkt_opts_t* opts, uint32_t p0, uint32_t n) {
+    // (a lane past the batch end may hold a zero record: status OK, l4 = 0, so a slice
+    // can come out "negative"; it is empty, as walk_options' `on` flags treat it)
+    const uint32_t t_nb = S.tcp && S.t_hi > S.t_lo ? S.t_hi - S.t_lo : 0u;
+    const uint32_t ip_nb = S.ip_parsed && S.ip_hi > S.ip_lo ? S.ip_hi - S.ip_lo : 0u;
+    // the partner frame q of this lane: rank by TCP bytes (desc) == q's rank by IPv4 bytes
+    // (asc); slices are at most 40 B (keys 0..10), the clamp keeps the ranks a permutation
+    const uint32_t rt = wave_rank11(min(t_nb >> 2, 10u), true);
+    const uint32_t ri = wave_rank11(min(ip_nb >> 2, 10u), false);
+    const int q = __builtin_amdgcn_ds_bpermute((int)(rt << 2),
+                                               __builtin_amdgcn_ds_permute((int)(ri << 2), lane));
+    const uint32_t ip_at = (uint32_t)__shfl((int)(slot_bias + S.ip_lo), q, kWave);
+    const uint32_t ip_n = (uint32_t)__shfl((int)ip_nb, q, kWave);
+    const bool ip_has = __shfl((int)S.ip_parsed, q, kWave) != 0;
+
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = 0;
+    uint32_t ip_end = 0;
+    // phase 0: this frame's TCP walk; 1: frame q's IPv4 walk; 2: done
+    uint32_t phase = S.tcp ? 0u : (ip_has ? 1u : 2u);
+    OptCur c;
+    c.base = c.at = phase == 0 ? slot_bias + S.t_lo : ip_at;
+    c.end = c.at + (phase == 0 ? t_nb : ip_n);
+    c.cnt = c.kinds = 0;
+    c.stop = RPKT_OPT_END;
+    c.trace = 0;
+    while (phase < 2u) {
+        const bool tcp = phase == 0u;
+        if (c.at < c.end) {
+            const uint32_t a = c.at & ~3u, sh = c.at & 3u;
+            const uint32_t R0 = lds32(win, a), R1 = lds32(win, a + 4u);
+            const uint32_t R2 = lds32(win, a + 8u), R3 = lds32(win, a + 12u);
+            const uint32_t d0 = align_bytes(R1, R0, sh);
+            const uint32_t t = d0 & 0xffu;
+            const uint32_t nrem = c.end - c.at;
+            if (t <= 1u) {                                     // EOL / NOP run
+                const uint32_t x = d0 ^ (t ? 0x01010101u : 0u);
+                uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+                k = k < nrem ? k : nrem;
+                c.kinds |= 1u << t;
+                const uint32_t nib = (t ? 0x2222u : 0x1111u) & ((1u << (4 * k)) - 1u);
+                if (c.cnt < 16) c.trace |= (uint64_t)nib << (4 * c.cnt);
+                c.cnt += k;
+                c.at += k;
+            } else {
+                const uint32_t rule = rules[(tcp ? 256u : 0u) + t];
+                const uint32_t hl = (d0 >> 8) & 0xffu;     // n >= 2 whenever a rule can pass
+                const uint32_t X = rule >> 4, kind = rule & 7u;
+                const bool fixed = (rule & 8u) != 0u;
+                const bool ok = (kind != 0u) & (nrem >= X) & (hl - X <= (fixed ? 0u : nrem - X));
+                if (!ok) {
+                    c.stop = kind == 0u ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
+                    c.end = c.at;
+                } else {
+                    const uint32_t d1 = align_bytes(R2, R1, sh), d2 = align_bytes(R3, R2, sh);
+                    const uint32_t g = kind | (tcp ? 8u : 0u);
+                    if (g == 2u) o[9] = (o[9] & 0xff000000u) | (d0 >> 8);
+                    if (g == 3u) o[8] = (o[8] & 0xffffu) | ((d0 >> 8) << 16);
+                    if (g == 4u) o[8] = (o[8] & 0xffff0000u) | be16_hi(d0);
+                    if (g == 5u) o[11] = bswap32(align_bytes(d1, d0, 2));
+                    if (g == 6u || g == 7u) {
+                        o[9] = (o[9] & 0x00ffffffu) | ((d0 >> 16) << 24);
+                        o[10] = bswap32(align_bytes(d1, d0, 3));
+                    }
+                    if (g == 10u) o[1] = (o[1] & 0xffffu) | (be16_hi(d0) << 16);
+                    if (g == 11u) o[0] = (o[0] & 0xff00ffffu) | (((d0 >> 16) & 0xffu) << 16);
+                    if (g == 13u) {
+                        o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) >> 3) << 24);
+                        o[4] = hl >= 6u ? bswap32(align_bytes(d1, d0, 2)) : 0u;
+                        o[5] = hl >= 10u ? bswap32(align_bytes(d2, d1, 2)) : 0u;
+                    }
+                    if (g == 14u) {
+                        o[2] = bswap32(align_bytes(d1, d0, 2));
+                        o[3] = bswap32(align_bytes(d2, d1, 2));
+                    }
+                    if (g == 15u) o[6] = (o[6] & 0xffff0000u) | hl;
+                    c.kinds |= 1u << kind;
+                    if (c.cnt < 16) c.trace |= (uint64_t)(kind + 1) << (4 * c.cnt);
+                    c.cnt += 1;
+                    c.at += fixed ? X : hl;
+                }
+            }
+        }
+        if (c.at >= c.end) {                                   // this walk ended
+            const uint32_t pos = c.at - c.base;
+            if (tcp) {
+                // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24;
+                // word 1: kinds | mss << 16; word 6: tcp_fo_len | tcp_end << 16
+                o[0] = (o[0] & 0xffff0000u) | c.cnt | (c.stop << 8);
+                o[1] = (o[1] & 0xffff0000u) | c.kinds;
+                o[6] = (o[6] & 0xff00ffffu) | (pos << 16);
+                o[12] = (uint32_t)c.trace;
+                o[13] = (uint32_t)(c.trace >> 32);
+                phase = ip_has ? 1u : 2u;
+                c.base = c.at = ip_at;
+                c.end = ip_at + ip_n;
+                c.cnt = c.kinds = 0;
+                c.stop = RPKT_OPT_END;
+                c.trace = 0;
+            } else {
+                // word 7: ip_count | ip_stop << 8 | ip_kinds << 16; ip_end: byte 27
+                ip_end = pos;
+                o[7] = c.cnt | (c.stop << 8) | (c.kinds << 16);
+                o[14] = (uint32_t)c.trace;
+                o[15] = (uint32_t)(c.trace >> 32);
+                phase = 2u;
+            }
+        }
+    }
+    // rows: this frame's TCP words, then frame q's IPv4 words (word 6's top byte last)
+    wave_sync();                                               // every walk has ended
+    uint32_t* st = reinterpret_cast<uint32_t*>(win);
+    uint32_t* me = st + lane * 17;
+    uint32_t* pq = st + q * 17;
+    me[0] = o[0]; me[1] = o[1]; me[2] = o[2]; me[3] = o[3]; me[4] = o[4]; me[5] = o[5];
+    me[6] = o[6]; me[12] = o[12]; me[13] = o[13];
+    pq[7] = o[7]; pq[8] = o[8]; pq[9] = o[9]; pq[10] = o[10]; pq[11] = o[11];
+    pq[14] = o[14]; pq[15] = o[15];
+    reinterpret_cast<uint8_t*>(pq)[27] = (uint8_t)ip_end;
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t cidx = k * kWave + lane, r = cidx / 4, pc = cidx % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[cidx]);
+    }
+}
+
+// A wave's 64 results staged through LDS `st` (stride 17 dwords: conflict-free) and
+// stored as 64-B rows, 4 KiB coalesced, with non-temporal stores.  `st` must not be
+// read by any lane of the wave after this call begins until it returns.
+__device__ __forceinline__ void store_opts(uint32_t* st, int lane, const uint32_t (&o)[16],
+                                           rpkt_opts_t* opts, uint32_t p0, uint32_t n) {
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
+    wave_sync();
+    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
+        const uint32_t* src = st + r * 17 + pc * 4;
+        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[c]);
+    }
+}
+
+}  // namespace

@@ -2,8 +2,75 @@
 // (mbuf chains), the flow-counter histogram and reduce, batched checksum::from_slice /
 // from_buf, and the streaming references tools/ablate.py times against the parse.
 #include "rpkt_common.h"
+#include "rpkt_opts.h"
+
+#include <mutex>
 
 namespace {
+
+// The option walks of parse_kernel<.., OPTS>: Ipv4OptionsIter / TcpOptionsIter over the
+// slices the parse just located, read from the header window in LDS.  The window holds
+// frame bytes [0, kWin - ph); a frame whose option bytes run past it (deep VLAN + IPv4
+// options + TCP options: up to byte 142 + 15 of phase) has its slot refilled, by the
+// wave's cooperative chunk mapping, with the 128 B from the 16-B chunk of its first
+// option byte (both slices span at most ihl4 + 40 <= 100 B); those lines were fetched
+// by the window and edge-line loads moments earlier, so the refill mostly hits L2.
+// Results leave through the window area (stride 17) before the records are staged
+// there.
+__device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buffer_rsrc_t rs,
+                                                    uint32_t fb, int lane, Frame fr,
+                                                    const LaneRec& L, const uint8_t* rules,
+                                                    rpkt_opts_t* opts, uint32_t p0, uint32_t n) {
+    const uint32_t* w = L.w;
+    const uint32_t l3 = w[16] & 0xffffu, l4 = w[16] >> 16;
+    const OptSlices S = opt_slices(L.status, (w[8] >> 8) & 0xffu, l3, l4,
+                                   ((w[14] >> 12) & 0xfu) * 4u);
+    const uint32_t ph = fr.off & 15u;
+    // every byte the walks use lies below need_hi (OptWin::dw's dword pair may read up to
+    // 7 B past it: window padding or the next slot, never used)
+    const bool over = S.need && S.need_hi + ph > (uint32_t)kWin;
+    uint32_t bias = ph;
+#ifndef RPKT_OPT_ABLATE
+#define RPKT_OPT_ABLATE 0        // development: 1 = no walks (zero results), 2 = no refill
+#endif
+    if (RPKT_OPT_ABLATE != 2 && __builtin_expect(__ballot(over) != 0, 1)) {   // wave-uniform
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        uint32_t fix = 0;
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) {
+            const int c = k * kWave + lane;
+            const int q = c / kWinChunks, j = c % kWinChunks;
+            const uint32_t lo = (uint32_t)__shfl((int)(over ? fr.off + S.need_lo : 0u), q, kWave);
+            const uint32_t hi = (uint32_t)__shfl((int)(over ? fr.off + S.need_hi : 0u), q, kWave);
+            const uint32_t a = (lo & ~15u) + 16u * j;
+            addr[k] = a < hi ? a : fb;
+            fix |= (uint32_t)straddles(addr[k], fb) << k;
+        }
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+        wave_sync();                                                // the parse's reads are done
+#pragma unroll
+        for (int k = 0; k < kWinChunks; ++k) {
+            u32x4 v = d[k];
+            if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+            if (addr[k] != fb) put_chunk(W, k * kWave + lane, v);
+        }
+        wave_sync();
+        if (over) bias = ((fr.off + S.need_lo) & 15u) - S.need_lo;
+    }
+#if RPKT_OPT_ABLATE == 1
+    uint32_t o[16] = {};
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+#elif RPKT_OPT_PAIRED
+    walk_options_paired(W.win, lane, lane * kSlot + bias, S, rules, opts, p0, n);
+#else
+    const OptWin s{&W.win[lane * kSlot], bias};
+    uint32_t o[16];
+    walk_options(s, S, rules, o);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+#endif
+}
 
 // One wavefront per 64-frame tile: window loads -> LDS, lane-per-frame parse,
 // flattened L4 stream, LDS-staged coalesced record stores.  (A persistent variant
@@ -21,13 +88,23 @@ namespace {
 // window loads without the L4 stream).
 // C16: write the 16-byte compact record (rpkt_rec16_t) instead of the 80-byte one:
 // kept in registers, one 16-B store per lane (1 KiB contiguous per wave), no LDS stage.
-template <bool L4, int V, bool C16 = false>
+// OPTS: also walk each frame's IPv4 and TCP options (rpkt_gpu_parse_options_batch) from
+// the header window the parse holds, between the parse and the L4 stream.
+template <bool L4, int V, bool C16 = false, bool OPTS = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                   uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
-                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets) {
+                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
+                  rpkt_opts_t* __restrict__ opts) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    // the option-type rules of both iterators (OPTS; 4 + 4 x 9744 + 512 B: still four
+    // blocks per CU)
+    __shared__ uint8_t opt_rules[OPTS ? 512 : 4];
+    if constexpr (OPTS) {
+        opt_rules_fill(opt_rules);
+        __syncthreads();
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     WaveScratch& W = scratch[wid];
@@ -76,6 +153,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     } else {
         parse_lane(W, lane, fr, valid, flags, L);
     }
+    if constexpr (OPTS) options_from_window(W, rs, frames_bytes, lane, fr, L, opt_rules, opts, p0, n);
     if constexpr (V != 3 && !C16) stage_record(W, lane, L.w);
 
     // 3. L4 bytes beyond the window: flattened chunk stream over the tile.  The stream
@@ -512,6 +590,64 @@ void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
     flush_records<true>(W, lane, recs, p0, n);
 }
 
+#ifdef RPKT_ABLATE
+// Wave-contiguous streaming references (the copy ceiling of bench.py): every wave owns
+// one contiguous slice of the input and one of the output, in 1-KiB units (64 lanes x
+// 16 B, one dwordx4 per lane per unit), reads its input slice four units at a time and
+// writes its output slice in proportion as it goes, so the read and write streams mix
+// at the in:out ratio throughout (1:1, or config 2's 64 B read : 80 B written per
+// frame).  AUX: load cache policy (2 = non-temporal); NTS: non-temporal stores.
+// COPY: the output is the input itself (memcpy; in16 == out16), else a value derived
+// from the loads (keeps them live).
+template <int AUX, bool NTS, bool COPY>
+__global__ __launch_bounds__(kWave * kWavesPerBlock)
+void wave_stream_ref_kernel(const uint8_t* __restrict__ in, uint32_t in16,
+                            u32x4* __restrict__ out, uint32_t out16) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t gw = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    const uint32_t in_u = in16 / kWave, out_u = out16 / kWave;
+    const uint32_t i0 = (uint32_t)((uint64_t)in_u * gw / nw), i1 = (uint32_t)((uint64_t)in_u * (gw + 1) / nw);
+    const uint32_t o0 = (uint32_t)((uint64_t)out_u * gw / nw), o1 = (uint32_t)((uint64_t)out_u * (gw + 1) / nw);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(in, in16 * 16u);
+    const uint32_t oob = in16 * 16u;
+    u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t o = o0;
+    for (uint32_t i = i0; i < i1; i += 4) {
+        u32x4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            x[u] = load16_fast<AUX>(rs, i + u < i1 ? ((i + u) * kWave + lane) * 16u : oob);
+        if constexpr (COPY) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (i + u < i1) {
+                    u32x4* dst = &out[(size_t)(i + u) * kWave + lane];
+                    if constexpr (NTS) __builtin_nontemporal_store(x[u], dst);
+                    else *dst = x[u];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc ^= x[u];
+            const uint32_t done = i + 4 < i1 ? i + 4 - i0 : i1 - i0;
+            const uint32_t due = o0 + (uint32_t)((uint64_t)(o1 - o0) * done / (i1 - i0));
+            for (; o < due; ++o) {
+                u32x4* dst = &out[(size_t)o * kWave + lane];
+                if constexpr (NTS) __builtin_nontemporal_store(acc + o, dst);
+                else *dst = acc + o;
+            }
+        }
+    }
+    if constexpr (!COPY) {
+        for (; o < o1; ++o) {
+            u32x4* dst = &out[(size_t)o * kWave + lane];
+            if constexpr (NTS) __builtin_nontemporal_store(acc + o, dst);
+            else *dst = acc + o;
+        }
+    }
+}
+
 // Streaming reference for the roofline: read `in16` 16-B chunks and write `out16`
 // chunks with plain coalesced dwordx4 accesses (what a perfect parse would move).
 template <int U, bool NT>
@@ -589,6 +725,8 @@ void tile_rw_ref_kernel(const uint8_t* __restrict__ frames, uint32_t frames_byte
         if (c / 5 < nrec) __builtin_nontemporal_store(acc + c, &out[(size_t)p0 * 5 + c]);
     }
 }
+
+#endif  // RPKT_ABLATE
 
 // ---- flow counters: LDS-privatised histogram per workgroup + slab reduce ----
 // One workgroup per CU-sized slice of the events; each keeps, per bucket in LDS, a
@@ -791,6 +929,41 @@ __global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
     out[p] = (uint16_t)fold16(acc);
 }
 
+// shared checks of the parse entry points
+int parse_args_ok(const rpkt_batch_t* b, uint32_t flags, const void* recs_dev,
+                         const void* flow_ev_dev, uint32_t n_buckets) {
+    if (!b || !recs_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)
+            return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    return 1;
+}
+
+template <bool C16>
+int parse_options(const rpkt_batch_t* b, uint32_t flags, void* recs_dev, rpkt_opts_t* opts_dev,
+                         rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
+    if (!opts_dev) return RPKT_E_INVAL;
+    const int ok = parse_args_ok(b, flags, recs_dev, flow_ev_dev, n_buckets);
+    if (ok != 1) return ok;
+    if (((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, C16, true>
+                                     : parse_kernel<false, 0, C16, true>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets, opts_dev);
+}
+
 }  // namespace
 
 // This unit compiles twice: as is (128-B windows) and with RPKT_PARSE_W64 (RPKT_WIN 64,
@@ -815,7 +988,8 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
     auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
-                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,
+                  (rpkt_opts_t*)nullptr);
 }
 #else
 int rpkt_gpu_parse_batch_compact_w64(const rpkt_batch_t*, uint32_t, rpkt_rec16_t*,
@@ -862,7 +1036,7 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0> : parse_kernel<false, 0>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
-                  recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+                  recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
 }
 
 int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,
@@ -887,7 +1061,21 @@ int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec
     auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
-                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets);
+                  (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,
+                  (rpkt_opts_t*)nullptr);
+}
+
+int rpkt_gpu_parse_options_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs_dev,
+                                 rpkt_opts_t* opts_dev, rpkt_flow_ev_t* flow_ev_dev,
+                                 uint32_t n_buckets, void* stream) {
+    return parse_options<false>(b, flags, recs_dev, opts_dev, flow_ev_dev, n_buckets, stream);
+}
+
+int rpkt_gpu_parse_options_batch_compact(const rpkt_batch_t* b, uint32_t flags,
+                                         rpkt_rec16_t* recs_dev, rpkt_opts_t* opts_dev,
+                                         rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets,
+                                         void* stream) {
+    return parse_options<true>(b, flags, recs_dev, opts_dev, flow_ev_dev, n_buckets, stream);
 }
 
 int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,
@@ -912,6 +1100,10 @@ int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* re
                   n_buckets);
 }
 
+#ifdef RPKT_ABLATE
+// Development hook (librpkt_gpu_ablate.so only, not part of include/rpkt_gpu.h): the
+// parse kernel's ablation variants and the streaming references, for tools/ablate.py,
+// tools/variant_check.py and bench.py's copy_ceiling.
 int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs, int variant,
                            void* stream) {
     if (!b || !recs || b->n == 0) return RPKT_E_INVAL;
@@ -922,7 +1114,8 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
 #define RPKT_V(v)                                                                       \
     launch((flags & RPKT_F_L4_SUM) ? parse_kernel<true, v> : parse_kernel<false, v>,   \
            dim3(grid), dim3(per_block), 0, st, b->frames_dev, (uint32_t)b->frames_bytes,   \
-           b->offsets_dev, b->stride, flen, b->n, flags, recs, (uint64_t*)nullptr, 0u)
+           b->offsets_dev, b->stride, flen, b->n, flags, recs, (uint64_t*)nullptr, 0u,      \
+           (rpkt_opts_t*)nullptr)
     switch (variant) {
         case 0: return RPKT_V(0);
         case 1: return RPKT_V(1);
@@ -959,6 +1152,24 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
             return launch(tile_rw_ref_kernel, dim3(grid), dim3(per_block), 0, st, b->frames_dev,
                           (uint32_t)b->frames_bytes, b->offsets_dev, b->stride * kWave, b->n,
                           (u32x4*)recs);
+        // wave-contiguous references: 16/17 the read:write mix of the batch (frames read,
+        // n x 80 B written) default / non-temporal, 18/19 a memcpy of the frames buffer
+        // into recs (frames_bytes of it) default / non-temporal
+        case 16: case 17: case 18: case 19: {
+            const uint32_t in16 = (uint32_t)(b->frames_bytes / 16);
+            const uint32_t out16 = variant >= 18 ? in16 : b->n * (RPKT_REC_BYTES / 16);
+            const dim3 g(1024), blk(kWave * kWavesPerBlock);     // 4096 waves: one per SIMD slot
+            switch (variant) {
+                case 16: return launch(wave_stream_ref_kernel<0, false, false>, g, blk, 0, st,
+                                       b->frames_dev, in16, (u32x4*)recs, out16);
+                case 17: return launch(wave_stream_ref_kernel<2, true, false>, g, blk, 0, st,
+                                       b->frames_dev, in16, (u32x4*)recs, out16);
+                case 18: return launch(wave_stream_ref_kernel<0, false, true>, g, blk, 0, st,
+                                       b->frames_dev, in16, (u32x4*)recs, out16);
+                default: return launch(wave_stream_ref_kernel<2, true, true>, g, blk, 0, st,
+                                       b->frames_dev, in16, (u32x4*)recs, out16);
+            }
+        }
         case 13:
             return launch(copy_ref_kernel<8, false>, dim3(8192), dim3(256), 0, st,
                           (const u32x4*)b->frames_dev, (uint32_t)(b->frames_bytes / 16),
@@ -966,6 +1177,26 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         default: return RPKT_E_INVAL;
     }
 #undef RPKT_V
+}
+
+#endif  // RPKT_ABLATE
+
+// The histogram's 98 KB of dynamic LDS needs hipFuncSetAttribute once per device (the
+// attribute belongs to the function on the current device).  Host threads may call the
+// ABI concurrently and a process may drive several GPUs (examples/flow_reduce.cpp), so
+// the flag is per device and set under a lock; a failed attempt is retried next call.
+static int flow_hist_attr_once() {
+    static std::mutex mu;
+    static uint64_t done[4] = {0, 0, 0, 0};          // bit d: device d (up to 256 devices)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 256) dev = 0;
+    std::lock_guard<std::mutex> g(mu);
+    if (done[dev >> 6] & (1ull << (dev & 63))) return RPKT_OK;
+    const int rc = hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+    if (rc == RPKT_OK) done[dev >> 6] |= 1ull << (dev & 63);
+    return rc;
 }
 
 size_t rpkt_gpu_flow_workspace_bytes(uint32_t n, uint32_t n_buckets) {
@@ -987,13 +1218,9 @@ int rpkt_gpu_flow_count(const rpkt_flow_ev_t* ev, uint32_t n, uint32_t n_buckets
     const uint32_t slabs = flow_blocks(n);
     const uint32_t per = (n + slabs - 1) / slabs;
     const size_t lds = 3 * (size_t)(n_buckets + 1) * sizeof(uint32_t);
-    static bool attr_set = false;
-    if (!attr_set) {
-        int rc0 = hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+    {
+        const int rc0 = flow_hist_attr_once();
         if (rc0) return rc0;
-        attr_set = true;
     }
     int rc = launch(flow_hist_kernel, dim3(slabs), dim3(kFlowThreads), lds, st,
                     (const uint64_t*)ev, n, per, n_buckets, (uint32_t*)workspace);

@@ -474,7 +474,9 @@ extern "C" {
 #ifndef RPKT_TX_W64
 int rpkt_gpu_build_batch_w64(const rpkt_batch_t*, const rpkt_rec_t*, uint32_t, uint8_t*, void*);
 int rpkt_gpu_forward_batch_w64(const rpkt_batch_t*, const rpkt_fwd_t*, uint8_t*, void*);
+#ifdef RPKT_ABLATE
 int rpkt_gpu_debug_forward_variant_w64(const rpkt_batch_t*, const rpkt_fwd_t*, uint8_t*, int, void*);
+#endif
 #endif
 
 #ifndef RPKT_TX_W64
@@ -528,7 +530,9 @@ int RPKT_TX_FN(rpkt_gpu_forward_batch)(const rpkt_batch_t* b, const rpkt_fwd_t* 
                   b->stride, flen, b->n, *fwd, keep_dev);
 }
 
-// Development hook (not part of include/rpkt_gpu.h): forward_kernel ablation variants.
+#ifdef RPKT_ABLATE
+// Development hook (librpkt_gpu_ablate.so only, not part of include/rpkt_gpu.h):
+// forward_kernel ablation variants for tools/ablate_fwd.py.
 int RPKT_TX_FN(rpkt_gpu_debug_forward_variant)(const rpkt_batch_t* b, const rpkt_fwd_t* fwd,
                                                uint8_t* keep_dev, int variant, void* stream) {
     if (!b || !fwd || !keep_dev || b->n == 0) return RPKT_E_INVAL;
@@ -562,5 +566,7 @@ int RPKT_TX_FN(rpkt_gpu_debug_forward_variant)(const rpkt_batch_t* b, const rpkt
     }
 #undef RPKT_FV
 }
+
+#endif  // RPKT_ABLATE
 
 }  // extern "C"

@@ -1,6 +1,7 @@
 // rpkt_walks.hip — per-frame walks over a batch: the IPv4/TCP option iterators and the
 // protocol-layer walk driven by the pktfmt-derived table.
 #include "rpkt_common.h"
+#include "rpkt_opts.h"
 #include "rpkt_proto_table.h"
 
 namespace {
@@ -9,8 +10,10 @@ namespace {
 // One wave per 64 frames.  The records give each frame's option slices; only the
 // 16-B chunks that overlap a slice are loaded (frames without options cost their
 // record read and the 64-B output only).  Lane-per-frame walk over LDS bytes with
-// the per-type parse rules of the generated option views (oracle/rpkt_oracle_opts.c
-// cites them); results staged through LDS and stored as 4 KiB of coalesced rows.
+// the per-type parse rules of the generated option views (rpkt_opts.h;
+// oracle/rpkt_oracle_opts.c cites them); results staged through LDS and stored as
+// 4 KiB of coalesced rows.  (rpkt_gpu_parse_options_batch runs the same walks inside
+// the parse, on the header window it already holds.)
 constexpr int kOptChunks = 8;                  // 128 B from the 16-B phase of the first
 constexpr int kOptSlot = 132;                  // option byte: both slices span at most
                                                // ihl4 + 40 <= 100 B, + 15 of phase
@@ -18,89 +21,6 @@ struct OptScratch {
     uint8_t win[kWave * kOptSlot];             // 8448 B (stride 33 dwords: conflict-free),
 };                                             // so four blocks (16 waves) fit a CU
 static_assert(kWave * 21 * 4 <= kWave * kOptSlot, "record stage fits the option window");
-
-// Option bytes in LDS: frame byte x of this lane at base[x + bias] (bias = the window's
-// phase minus the first option byte's frame offset; only x >= that offset is read).
-struct OptWin {
-    const uint8_t* base;                       // the lane's slot (4-aligned)
-    uint32_t bias;
-    __device__ __forceinline__ uint32_t b(uint32_t x) const { return base[x + bias]; }
-    // frame bytes x..x+3, little-endian: two aligned LDS dwords and a byte align
-    __device__ __forceinline__ uint32_t dw(uint32_t x) const {
-        const uint32_t y = x + bias, a = y & ~3u;
-        return align_bytes(lds32(base, a + 4), lds32(base, a), y & 3u);
-    }
-    __device__ __forceinline__ uint32_t be16(uint32_t x) const { return be16_lo(dw(x)); }
-    __device__ __forceinline__ uint32_t be32(uint32_t x) const { return bswap32(dw(x)); }
-};
-
-// The per-type parse rules of the generated option views (TcpOptionsIter over
-// tcp/generated.rs, Ipv4OptionsIter over ipv4/generated.rs; oracle/rpkt_oracle_opts.c
-// cites them), as a table per option type read from LDS in the walk (a per-lane type
-// would make a switch divergent): kind index (2..7; 0: not an option type of this
-// iterator) | fixed << 3 | x << 4, where the option needs n >= x remaining bytes and
-// header_len == x (fixed) or x <= header_len <= n.  Types 0 (EOL) and 1 (NOP), kinds
-// 0 and 1 of both iterators, are length-1 options consumed by opt_run.
-__device__ inline uint32_t opt_rule(bool tcp, uint32_t t) {
-    if (tcp) {
-        switch (t) {
-            case 2: return 2u | 8u | 4u << 4;      // Mss
-            case 3: return 3u | 8u | 3u << 4;      // WindowScale
-            case 4: return 4u | 8u | 2u << 4;      // SackPermitted
-            case 5: return 5u | 2u << 4;           // Sack
-            case 8: return 6u | 8u | 10u << 4;     // Timestamp
-            case 34: return 7u | 2u << 4;          // FastOpen
-            default: return 0u;
-        }
-    }
-    switch (t) {
-        case 68: return 2u | 4u << 4;              // Timestamp
-        case 7: return 3u | 3u << 4;               // RecordRoute
-        case 148: return 4u | 8u | 4u << 4;        // RouteAlert
-        case 134: return 5u | 6u << 4;             // CommercialSecurity
-        case 137: return 6u | 8u | 7u << 4;        // StrictSourceRoute
-        case 131: return 7u | 8u | 7u << 4;        // LooseSourceRoute
-        default: return 0u;
-    }
-}
-// option length (> 0), 0 = the type's parse fails (malformed), -1 = unknown type
-__device__ __forceinline__ int opt_len(uint32_t rule, uint32_t d0, uint32_t n, int& kind) {
-    const uint32_t hl = n >= 2 ? (d0 >> 8) & 0xffu : 0u;
-    const uint32_t x = rule >> 4;
-    const bool fixed = (rule & 8u) != 0u;
-    const bool ok = (n >= x) & (fixed ? hl == x : (hl >= x) & (hl <= n));
-    kind = (int)(rule & 7u);
-    return (rule & 7u) == 0u ? -1 : (ok ? (int)(fixed ? x : hl) : 0);
-}
-
-// One step of a TLV walk (state of Ipv4OptionsIter / TcpOptionsIter): the two walks of
-// a frame are independent, so the kernel steps both in one loop and their LDS round
-// trips overlap.
-struct OptWalk {
-    uint32_t lo, nb, pos, cnt, kinds, stop;
-    uint64_t trace;
-    bool on;
-};
-
-// A run of one-byte options of one type (EOL = kind 0, NOP = kind 1 in both iterators:
-// each is an option of length 1 and the walk goes on) is consumed up to four at a
-// time from the dword at the cursor: padding runs are most of a walk's steps.
-__device__ __forceinline__ bool opt_run(OptWalk& w, uint32_t d0) {
-    const uint32_t t0 = d0 & 0xffu;
-    if (t0 > 1u) return false;
-    const uint32_t x = d0 ^ (t0 ? 0x01010101u : 0u);   // zero bytes: the same type
-    uint32_t k = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
-    k = k < w.nb - w.pos ? k : w.nb - w.pos;            // >= 1: byte 0 matches
-    w.kinds |= 1u << t0;
-    if (w.cnt < 16) {
-        const uint32_t nib = (t0 ? 0x2222u : 0x1111u) & ((1u << (4 * k)) - 1u);   // k <= 4
-        w.trace |= (uint64_t)nib << (4 * w.cnt);
-    }
-    w.cnt += k;
-    w.pos += k;
-    w.on = w.pos < w.nb;
-    return true;
-}
 
 // C16: the records are rpkt_rec16_t (16 B: one coalesced dwordx4 per lane) instead of
 // rpkt_rec_t (80 B, staged through LDS); the walks need status, IP protocol, l3, l4 and
@@ -112,12 +32,8 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     uint32_t n, const void* __restrict__ recs_any, rpkt_opts_t* __restrict__ opts) {
     __shared__ __attribute__((aligned(16))) OptScratch scratch[kWavesPerBlock];
     // the option-type rules of both iterators (a per-lane type: LDS, not a switch)
-    __shared__ uint8_t rules[2][256];
-    static_assert(kWave * kWavesPerBlock >= 256, "one fill pass");
-    if (threadIdx.x < 256) {
-        rules[0][threadIdx.x] = (uint8_t)opt_rule(false, threadIdx.x);
-        rules[1][threadIdx.x] = (uint8_t)opt_rule(true, threadIdx.x);
-    }
+    __shared__ uint8_t rules[512];
+    opt_rules_fill(rules);
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
@@ -170,14 +86,9 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         l4 = w16 >> 16;
         doff4 = ((w14 >> 12) & 0xfu) * 4u;
     }
-    const bool ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
-    const bool tcp = status == RPKT_S_OK && proto == 6u;
-    const uint32_t ip_lo = l3 + 20u, ip_hi = ip_parsed ? l4 : ip_lo;
-    const uint32_t t_lo = l4 + 20u, t_hi = tcp ? l4 + doff4 : t_lo;
-    // option bytes needed: [lo, hi) of the frame (both slices); chunks outside it skip
-    const uint32_t need_lo = ip_hi > ip_lo ? ip_lo : t_lo;
-    const uint32_t need_hi = t_hi > t_lo ? t_hi : ip_hi;
-    const bool need = (ip_hi > ip_lo) || (t_hi > t_lo);
+    const OptSlices S = opt_slices(status, proto, l3, l4, doff4);
+    const uint32_t need_lo = S.need_lo, need_hi = S.need_hi;
+    const bool need = S.need;
 
     // window chunks that overlap the option bytes -> LDS slots
     {
@@ -211,102 +122,15 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
     wave_sync();
 
-    // the two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
-    // TcpOptionsIter::next, tcp/generated.rs:1400-1484), stepped together
+#if RPKT_OPT_PAIRED
+    walk_options_paired(W.win, lane, lane * kOptSlot + (((fr.off + need_lo) & 15u) - need_lo), S,
+                        rules, opts, p0, n);
+#else
     const OptWin s{&W.win[lane * kOptSlot], ((fr.off + need_lo) & 15u) - need_lo};
     uint32_t o[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) o[k] = 0;
-    OptWalk ip{ip_lo, ip_hi - ip_lo, 0, 0, 0, RPKT_OPT_END, 0, ip_parsed && ip_hi > ip_lo};
-    OptWalk tw{t_lo, t_hi - t_lo, 0, 0, 0, RPKT_OPT_END, 0, tcp && t_hi > t_lo};
-    while (ip.on || tw.on) {
-        if (ip.on) {
-            const uint32_t at = ip.lo + ip.pos;
-            const uint32_t d0 = s.dw(at);
-            int kind = 0;
-            const int used = opt_run(ip, d0) ? -2 : opt_len(rules[0][d0 & 0xffu], d0, ip.nb - ip.pos, kind);
-            if (used == -2) {
-            } else if (used <= 0) {
-                ip.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
-                ip.on = false;
-            } else {
-                if (kind == 2) o[9] = (o[9] & 0xff000000u) | (d0 >> 8);
-                if (kind == 3) o[8] = (o[8] & 0xffffu) | ((d0 >> 8) << 16);
-                if (kind == 4) o[8] = (o[8] & 0xffff0000u) | be16_hi(d0);
-                if (kind == 5) o[11] = s.be32(at + 2);
-                if (kind == 6 || kind == 7) {
-                    o[9] = (o[9] & 0x00ffffffu) | ((d0 >> 16) << 24);
-                    o[10] = s.be32(at + 3);
-                }
-                ip.kinds |= 1u << kind;
-                if (ip.cnt < 16) ip.trace |= (uint64_t)(kind + 1) << (4 * ip.cnt);
-                ip.cnt += 1;
-                ip.pos += (uint32_t)used;
-                ip.on = ip.pos < ip.nb;
-            }
-        }
-        if (tw.on) {
-            const uint32_t at = tw.lo + tw.pos;
-            const uint32_t d0 = s.dw(at);
-            int kind = 0;
-            const int used = opt_run(tw, d0) ? -2 : opt_len(rules[1][d0 & 0xffu], d0, tw.nb - tw.pos, kind);
-            if (used == -2) {
-            } else if (used <= 0) {
-                tw.stop = used < 0 ? RPKT_OPT_UNKNOWN : RPKT_OPT_MALFORMED;
-                tw.on = false;
-            } else {
-                if (kind == 2) o[1] = (o[1] & 0xffffu) | (be16_hi(d0) << 16);
-                if (kind == 3) o[0] = (o[0] & 0xff00ffffu) | (((d0 >> 16) & 0xffu) << 16);
-                if (kind == 5) {
-                    const uint32_t hl = (d0 >> 8) & 0xffu;
-                    o[0] = (o[0] & 0x00ffffffu) | (((hl - 2u) / 8u) << 24);
-                    o[4] = hl >= 6u ? s.be32(at + 2) : 0u;
-                    o[5] = hl >= 10u ? s.be32(at + 6) : 0u;
-                }
-                if (kind == 6) {
-                    o[2] = s.be32(at + 2);
-                    o[3] = s.be32(at + 6);
-                }
-                if (kind == 7) o[6] = (o[6] & 0xffff0000u) | ((d0 >> 8) & 0xffu);
-                tw.kinds |= 1u << kind;
-                if (tw.cnt < 16) tw.trace |= (uint64_t)(kind + 1) << (4 * tw.cnt);
-                tw.cnt += 1;
-                tw.pos += (uint32_t)used;
-                tw.on = tw.pos < tw.nb;
-            }
-        }
-    }
-    if (ip_parsed) {
-        // word 6: tcp_fo_len | tcp_end << 16 | ip_end << 24; word 7: ip_count | ip_stop << 8 | ip_kinds << 16
-        o[6] |= ip.pos << 24;
-        o[7] = ip.cnt | (ip.stop << 8) | (ip.kinds << 16);
-    }
-    if (tcp) {
-        // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24; word 1: kinds | mss << 16
-        o[0] = (o[0] & 0xffff0000u) | tw.cnt | (tw.stop << 8);
-        o[1] = (o[1] & 0xffff0000u) | tw.kinds;
-        o[6] = (o[6] & 0xff00ffffu) | (tw.pos << 16);
-    }
-    const uint64_t tcp_trace = tw.trace, ip_trace = ip.trace;
-    o[12] = (uint32_t)tcp_trace;
-    o[13] = (uint32_t)(tcp_trace >> 32);
-    o[14] = (uint32_t)ip_trace;
-    o[15] = (uint32_t)(ip_trace >> 32);
-
-    // stage (stride 17 dwords) and store 64 rows of 64 B coalesced
-    wave_sync();
-    uint32_t* st = reinterpret_cast<uint32_t*>(W.win);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
-    wave_sync();
-    const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
-    u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t c = k * kWave + lane, r = c / 4, pc = c % 4;
-        const uint32_t* src = st + r * 17 + pc * 4;
-        if (r < nrow) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[c]);
-    }
+    walk_options(s, S, rules, o);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+#endif
 }
 
 // ---- protocol layer walk: the pktfmt-derived table interpreted per frame ----
@@ -1015,7 +839,8 @@ int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void
     return launch_layers<kLayFrames, true>(b, flen, layers_dev, stream);
 }
 
-// Development hook (not part of include/rpkt_gpu.h): the walk with F frames per lane
+#ifdef RPKT_ABLATE
+// Development hook (librpkt_gpu_ablate.so only: the walk with F frames per lane
 // (1, 2, 4, 8), for timing the choice of kLayFrames.  (Tried and dropped, DESIGN.md:
 // prefetching a lane's next frame window into registers, 84 -> 90 us; per-group steps
 // specialised at compile time and run one uniform group after another, 84 -> 195 us
@@ -1038,7 +863,6 @@ int rpkt_gpu_debug_layers_variant(const rpkt_batch_t* b, rpkt_layers_t* layers_d
     }
 }
 
-// Development hook (not part of include/rpkt_gpu.h): ablation variants of the parse
-// kernel and the streaming-copy roofline reference, for tools/ablate.py.
+#endif  // RPKT_ABLATE
 
 }  // extern "C"

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-from .build import GPU_LIB
+from .build import ABLATE_LIB, GPU_LIB
 from .records import LAYERS_BYTES, OPTS_BYTES, REC_BYTES, REC16_BYTES, F_FLOW_EV
 
 RPKT_OK = 0
@@ -51,7 +51,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_chains", "rpkt_gpu_build_batch", "rpkt_gpu_forward_batch",
            "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch",
            "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
-           "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact"]
+           "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact",
+           "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact"]
 
 _lib = None
 
@@ -111,6 +112,13 @@ def lib():
         L.rpkt_gpu_options_batch_compact.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                                      ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_options_batch_compact.restype = ctypes.c_int
+        L.rpkt_gpu_parse_options_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_uint32,
+                                                   ctypes.c_void_p, ctypes.c_void_p,
+                                                   ctypes.c_void_p, ctypes.c_uint32,
+                                                   ctypes.c_void_p]
+        L.rpkt_gpu_parse_options_batch.restype = ctypes.c_int
+        L.rpkt_gpu_parse_options_batch_compact.argtypes = L.rpkt_gpu_parse_options_batch.argtypes
+        L.rpkt_gpu_parse_options_batch_compact.restype = ctypes.c_int
         L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.rpkt_gpu_layers_batch.restype = ctypes.c_int
@@ -128,6 +136,22 @@ def lib():
         L.rpkt_flow_hash.restype = ctypes.c_uint32
         _lib = L
     return _lib
+
+
+_ablate = None
+
+
+def ablate_lib():
+    """librpkt_gpu_ablate.so: the product entry points plus the development hooks
+    (rpkt_gpu_debug_*: kernel ablation variants and streaming references) that tools/
+    and bench.py's copy ceiling use.  Never used by the product path."""
+    global _ablate
+    if _ablate is None:
+        lib()                                   # torch's HIP runtime first, as for lib()
+        if not os.path.exists(ABLATE_LIB):
+            raise RpktError("development library not built: %s missing" % ABLATE_LIB)
+        _ablate = ctypes.CDLL(ABLATE_LIB)
+    return _ablate
 
 
 def device_info():
@@ -396,6 +420,29 @@ def options_batch(batch, recs, opts=None, stream=None, compact=False):
     rc = fn(ctypes.byref(d), recs.data_ptr(), opts.data_ptr(), _stream_ptr(stream))
     _check(rc, "rpkt_gpu_options_batch_compact" if compact else "rpkt_gpu_options_batch")
     return opts
+
+
+def parse_options_batch(batch, flags=3, recs=None, opts=None, flow_ev=None, n_buckets=0,
+                        stream=None, compact=False):
+    """rpkt_gpu_parse_options_batch[_compact]: the parse and both option walks in one
+    pass.  Returns (records, opts) -- n * 80 (or 16, compact) and n * 64 bytes, uint8 --
+    plus the flow events when RPKT_F_FLOW_EV is set."""
+    torch = _torch()
+    dev = batch.frames.device
+    if recs is None:
+        recs = torch.empty(batch.n * (REC16_BYTES if compact else REC_BYTES), dtype=torch.uint8,
+                           device=dev)
+    if opts is None:
+        opts = torch.empty(batch.n * OPTS_BYTES, dtype=torch.uint8, device=dev)
+    if flags & F_FLOW_EV and flow_ev is None:
+        flow_ev = torch.empty(batch.n, dtype=torch.int64, device=dev)
+    d = batch.desc()
+    fn = (lib().rpkt_gpu_parse_options_batch_compact if compact
+          else lib().rpkt_gpu_parse_options_batch)
+    rc = fn(ctypes.byref(d), flags, recs.data_ptr(), opts.data_ptr(),
+            flow_ev.data_ptr() if flow_ev is not None else None, n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_options_batch%s" % ("_compact" if compact else ""))
+    return (recs, opts, flow_ev) if flags & F_FLOW_EV else (recs, opts)
 
 
 def layers_batch(batch, out=None, stream=None):

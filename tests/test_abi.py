@@ -33,6 +33,35 @@ def test_every_declared_symbol_is_exported(L):
     assert sorted(engine.EXPORTS) == names
 
 
+def dynamic_exports(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if ln.split()[-1].startswith("rpkt_")})
+
+
+def test_product_library_exports_exactly_the_header(L):
+    """The product library's rpkt_* exports are the header's declarations, no more: the
+    kernel ablation variants and streaming references live in librpkt_gpu_ablate.so."""
+    from rpkt_amd.build import ABLATE_LIB, GPU_LIB
+    assert dynamic_exports(GPU_LIB) == declared_functions()
+    dev = dynamic_exports(ABLATE_LIB)
+    assert set(declared_functions()) < set(dev)
+    assert {"rpkt_gpu_debug_variant", "rpkt_gpu_debug_forward_variant",
+            "rpkt_gpu_debug_layers_variant"} <= set(dev)
+
+
+def test_library_loads_without_rccl(L):
+    """RCCL is resolved when the collective is first used (rpkt_coll.hip), so a parse-only
+    host needs no librccl to load the engine."""
+    import subprocess
+    from rpkt_amd.build import GPU_LIB
+    out = subprocess.run(["readelf", "-d", GPU_LIB], capture_output=True, text=True,
+                         check=True).stdout
+    assert "rccl" not in out
+    assert isinstance(L.rpkt_gpu_coll_version(), int)
+
+
 def test_abi_version_and_info(L):
     assert L.rpkt_gpu_abi_version() == 1
     assert b"gfx950" in L.rpkt_gpu_build_info()

@@ -33,7 +33,7 @@ def _worker(rank, world, port, out):
     _, ev = oracle.parse_batch(hb.frames, hb.n, flags=3, offsets=hb.offsets, n_buckets=NB,
                                flow_ev=True)
     c = torch.from_numpy(oracle.flow_count(ev, NB).view(np.int64).copy())
-    rd.reduce_counters(c)
+    assert rd.reduce_counters(c) is c and rd.last_reduce_path == "gloo"
     if rank == 0:
         np.save(out, c.numpy())
     dist.barrier()
@@ -61,3 +61,26 @@ def test_shard_ranges_partition():
             assert r[0][0] == 0 and r[-1][1] == n
             assert all(r[k][1] == r[k + 1][0] for k in range(w - 1))
             assert max(b - a for a, b in r) - min(b - a for a, b in r) <= 1
+
+
+def _agree_worker(rank, world, port, flags, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rpkt_amd import dist as rd
+    got = rd.agree(flags[rank])
+    with open("%s.%d" % (out, rank), "w") as fh:
+        fh.write("1" if got else "0")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("flags", [(True, True), (True, False), (False, True), (True, True, False)])
+def test_reduce_path_is_decided_for_the_whole_group(tmp_path, flags):
+    """dist.agree (the C-ABI-reduce decision): every rank gets the same answer, True only
+    when every rank can take the RCCL path, so a rank-local refusal never splits the
+    ranks between ncclAllReduce and torch's all_reduce."""
+    out = str(tmp_path / "agree")
+    world = len(flags)
+    mp.spawn(_agree_worker, args=(world, _free_port(), flags, out), nprocs=world, join=True)
+    got = {open("%s.%d" % (out, r)).read() for r in range(world)}
+    assert got == {"1" if all(flags) else "0"}

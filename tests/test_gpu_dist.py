@@ -42,7 +42,8 @@ def _worker(rank, world, port, out):
     db = engine.DeviceBatch.from_host(hb)
     _, ev = engine.parse_batch(db, 3 | 4, n_buckets=NB)
     c = engine.flow_count(ev, hb.n, NB)
-    via = rd.reduce_counters(c, NB)
+    rd.reduce_counters(c, n_buckets=NB)
+    via = rd.last_reduce_path
     torch.cuda.synchronize()
     if rank == 0:
         np.save(out, c.cpu().numpy())
@@ -125,3 +126,46 @@ def test_flow_reduce_on_torch_rccl_communicator(tmp_path):
                        timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "rccl ok" in r.stdout
+
+
+THREADS_SCRIPT = r"""
+import sys, threading
+sys.path.insert(0, %r)
+import numpy as np, torch
+from rpkt_amd import engine, gen
+from oracle import oracle
+torch.cuda.set_device(0)
+NB = 8192
+hbs = [gen.make_batch(4, 200000, seed=40 + t) for t in range(2)]
+dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
+evs = [engine.parse_batch(d, 3 | 4, n_buckets=NB)[1] for d in dbs]
+torch.cuda.synchronize()
+go = threading.Barrier(2)
+out = [None, None]
+def run(t):
+    s = torch.cuda.Stream()
+    go.wait()                  # both threads make the process's first flow_count call at once
+    c = engine.flow_count(evs[t], hbs[t].n, NB, stream=s)
+    s.synchronize()
+    out[t] = c.cpu().numpy().view(np.uint64)
+th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+[x.start() for x in th]
+[x.join() for x in th]
+for t in range(2):
+    _, ev = oracle.parse_batch(hbs[t].frames, hbs[t].n, flags=3, offsets=hbs[t].offsets,
+                               n_buckets=NB, flow_ev=True)
+    assert np.array_equal(out[t], oracle.flow_count(ev, NB)), t
+print("threads ok")
+"""
+
+
+def test_flow_count_from_two_host_threads(tmp_path):
+    """Two host threads make the process's first rpkt_gpu_flow_count calls at the same time
+    on their own streams (the per-device, locked one-time LDS attribute setup); both
+    counter sets equal the oracle's."""
+    script = tmp_path / "threads.py"
+    script.write_text(THREADS_SCRIPT % ROOT)
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True,
+                       timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "threads ok" in r.stdout

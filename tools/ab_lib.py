@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3]
+Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3]
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -90,6 +90,17 @@ def main():
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
             call[name] = (lambda k, L=L, out=out: L.rpkt_gpu_options_batch_compact(
                 ctypes.byref(descs[k % R]), r16[k % R].data_ptr(), out.data_ptr(), sp))
+        elif mode in ("popts", "poptsc"):           # fused parse + option walks
+            fn = L.rpkt_gpu_parse_options_batch_compact if mode == "poptsc" else \
+                L.rpkt_gpu_parse_options_batch
+            fn.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_uint32, ctypes.c_void_p]
+            rec = torch.zeros(hb.n * (16 if mode == "poptsc" else 80), dtype=torch.uint8,
+                              device="cuda")
+            out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
+            outs[name + "_recs"] = rec
+            call[name] = (lambda k, fn=fn, out=out, rec=rec: fn(
+                ctypes.byref(descs[k % R]), 3, rec.data_ptr(), out.data_ptr(), None, 0, sp))
         elif mode == "layers":
             L.rpkt_gpu_layers_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p]
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")

@@ -27,7 +27,7 @@ ap.add_argument("--variants", default="0,1,2,3,10")
 ap.add_argument("--rotate", type=int, default=8, help="distinct batches rotated at config 2")
 args = ap.parse_args()
 
-L = engine.lib()
+L = engine.ablate_lib()      # the rpkt_gpu_debug_* hooks live in the development library
 L.rpkt_gpu_debug_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_variant.restype = ctypes.c_int

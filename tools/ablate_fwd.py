@@ -23,7 +23,7 @@ ap.add_argument("--launches", type=int, default=20)
 ap.add_argument("--variants", default="0,1,2,3")
 args = ap.parse_args()
 
-L = engine.lib()
+L = engine.ablate_lib()      # the rpkt_gpu_debug_* hooks live in the development library
 L.rpkt_gpu_debug_forward_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.POINTER(engine.Fwd),
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_forward_variant.restype = ctypes.c_int

@@ -25,7 +25,7 @@ ap.add_argument("--n", type=int, default=0)
 ap.add_argument("--config", type=int, default=9, help="9 = the capture mix, else a bench config")
 args = ap.parse_args()
 
-L = engine.lib()
+L = engine.ablate_lib()      # the rpkt_gpu_debug_* hooks live in the development library
 L.rpkt_gpu_debug_layers_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_void_p,
                                             ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_layers_variant.restype = ctypes.c_int

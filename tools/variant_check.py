@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="3,4,5,6")
 ap.add_argument("--variants", default="40")
 args = ap.parse_args()
-L = engine.lib()
+L = engine.ablate_lib()      # the rpkt_gpu_debug_* hooks live in the development library
 L.rpkt_gpu_debug_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_uint32,
                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
 L.rpkt_gpu_debug_variant.restype = ctypes.c_int
