@@ -529,12 +529,38 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
     return out
 
 
+# host-inclusive pipeline shape per config: device slots and 1M-frame batches per copy
+# (tools/host_rate.py sweeps them; profiles/r03_host/)
+HOST_SHAPE = {2: (3, 4), 3: (3, 1), 4: (3, 1)}
+
+
+def run_host(args):
+    """The path from and to host memory (north_star): pinned
+    hipMemcpyAsync H2D of the frames, the parse, D2H of the records, pipelined on three
+    streams (rpkt_amd.pipeline), with 80-B and 16-B records.  PCIe-bound; never the
+    headline value."""
+    from rpkt_amd import pipeline
+    out = {}
+    for c in [int(x) for x in args.host.split(",") if x.strip()]:
+        slots, group = HOST_SHAPE.get(c, (3, 1))
+        for compact in (False, True):
+            r = pipeline.host_inclusive(c, compact, slots=slots, group=group)
+            out["config%d%s" % (c, "_compact" if compact else "")] = {
+                k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+            torch.cuda.empty_cache()
+    return out
+
+
 def copy_ceiling(dbs, recs, steps):
     """Measured device-to-device copy ceilings beside config 2, same
-    stream and event timing as the parse: (1) a grid-stride copy kernel moving config 2's
-    own bytes (the 8 rotated 64 MiB frame buffers read, 80 MiB of records written:
-    rpkt_gpu_debug_variant 13, tools/ablate.py's v13); (2) hipMemcpyAsync device to
-    device of 1 GiB (torch copy_), read + written bytes counted."""
+    stream and event timing as the parse (development library's streaming references):
+      wave_mix / wave_mix_nt: wave-contiguous 16-B/lane streams of config 2's own bytes
+        (the 8 rotated 64 MiB frame buffers read, 80 MiB of records written at the
+        64 : 80 ratio throughout), default / non-temporal policy (variants 16 / 17);
+      wave_copy / wave_copy_nt: the same kernel as a 1:1 memcpy of 1 GiB (18 / 19);
+      same_mix_copy: the round-2 grid-stride copy of config 2's bytes (variant 13);
+      d2d_memcpy: hipMemcpyAsync device to device of 1 GiB (torch copy_).
+    Read + written bytes are counted."""
     L = engine.ablate_lib()               # the streaming references: development library
     L.rpkt_gpu_debug_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
@@ -555,23 +581,37 @@ def copy_ceiling(dbs, recs, steps):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / k / 1e3                     # seconds per launch
 
-    def mix(j):
-        rc = L.rpkt_gpu_debug_variant(ctypes.byref(descs[j % R]), 1, recs[j % R].data_ptr(), 13, sp)
-        if rc:
-            raise engine.RpktError("copy reference: rc %d" % rc)
-    t_mix = timed(mix, max(steps, 2 * R))
+    def variant(v, ds, outs):
+        def run(j):
+            rc = L.rpkt_gpu_debug_variant(ctypes.byref(ds[j % len(ds)]), 1,
+                                          outs[j % len(outs)].data_ptr(), v, sp)
+            if rc:
+                raise engine.RpktError("copy reference %d: rc %d" % (v, rc))
+        return run
+
+    def entry(t, nbytes, what):
+        return {"gb_per_s": round(nbytes / t / 1e9, 1), "us": round(t * 1e6, 2),
+                "bytes": int(nbytes), "what": what}
+
+    out = {}
+    k = max(steps, 2 * R)
     mix_bytes = dbs[0].frames.numel() + recs[0].numel()
+    mix_what = ("config 2's bytes: 64 MiB frames read, 80 MiB records written, 8 rotated "
+                "batches, ")
+    for name, v, what in (("wave_mix", 16, "wave-contiguous 16-B/lane, default policy"),
+                          ("wave_mix_nt", 17, "wave-contiguous 16-B/lane, non-temporal"),
+                          ("same_mix_copy", 13, "grid-stride copy (round 2's reference)")):
+        out[name] = entry(timed(variant(v, descs, recs), k), mix_bytes, mix_what + what)
     a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
     b = torch.empty_like(a)
-    t_d2d = timed(lambda j: b.copy_(a), 10)
+    big = [engine.Batch(a.data_ptr(), a.numel(), None, 64, 64, 1, 0)]
+    for name, v, what in (("wave_copy", 18, "default policy"), ("wave_copy_nt", 19, "non-temporal")):
+        out[name] = entry(timed(variant(v, big, [b]), 10), 2 * (1 << 30),
+                          "wave-contiguous 16-B/lane memcpy of 1 GiB (read + write), " + what)
+    out["d2d_memcpy"] = entry(timed(lambda j: b.copy_(a), 10), 2 * (1 << 30),
+                              "hipMemcpyAsync device to device, 1 GiB (read + write)")
     del a, b
-    return {"same_mix_copy": {"gb_per_s": round(mix_bytes / t_mix / 1e9, 1),
-                              "us": round(t_mix * 1e6, 2), "bytes": int(mix_bytes),
-                              "what": "grid-stride copy of config 2's bytes: 64 MiB frames read, "
-                                      "80 MiB records written, 8 rotated batches"},
-            "d2d_memcpy": {"gb_per_s": round(2 * (1 << 30) / t_d2d / 1e9, 1),
-                           "us": round(t_d2d * 1e6, 1), "bytes": 2 * (1 << 30),
-                           "what": "hipMemcpyAsync device to device, 1 GiB (read + write)"}}
+    return out
 
 
 FORBID_IPS = ["192.168.5.%d" % k for k in range(3, 11)]    # loopback_rx.rs:42-51
@@ -745,6 +785,9 @@ def main():
                     help="main leg as the fused parse + option walks (profiling it alone)")
     ap.add_argument("--compact", default="2,3",
                     help="configs also timed with 16-B compact records (extra.config<N>_compact)")
+    ap.add_argument("--host", default="2,3",
+                    help="configs also timed host-inclusive at N=1 (pinned H2D frames -> parse "
+                         "-> D2H records, rpkt_amd.pipeline): extra.host_inclusive")
     ap.add_argument("--strong", default="2,3",
                     help="configs also timed as one batch split over the ranks "
                          "(extra.config<N>_strong)")
@@ -806,6 +849,8 @@ def main():
         extra["config%d_opts" % c] = run_config(c, args, rank, world, opts=True)
         extra["config%d_opts_compact" % c] = run_config(c, args, rank, world, compact=True,
                                                         opts=True)
+    if world == 1 and args.host.strip():
+        extra["host_inclusive"] = run_host(args)
     if want_cpu and not args.no_config1:
         extra["config1"] = run_config1(args)
 

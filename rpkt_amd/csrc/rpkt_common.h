@@ -409,6 +409,11 @@ template <int AUX = 0>
 __device__ __forceinline__ EdgeLines edge_lines_window(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
                                                        WaveScratch& W, int lane, Frame fr,
                                                        bool valid, uint32_t min_tile_stream) {
+    // the cooperative mapping below gives each frame 8 lanes for kWinChunks passes, so it
+    // covers all 64 frames only with 128-B windows (8 chunks); the 64-B-window compiles
+    // take only batches whose frames lie inside their windows (nothing streams), so they
+    // never need the edge lines
+    if constexpr (kWinChunks != 8) return EdgeLines{false, 0u, 0u, 0u};
     {
         const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
         const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;

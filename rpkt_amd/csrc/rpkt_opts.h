@@ -11,6 +11,9 @@
 #ifndef RPKT_OPT_PAIRED
 #define RPKT_OPT_PAIRED 1        // 0: both walks of a frame stepped together (walk_options)
 #endif
+#ifndef RPKT_OPT_DEFER
+#define RPKT_OPT_DEFER 1         // 0: the paired walk with the getters updated every step
+#endif
 
 namespace {
 
@@ -53,6 +56,26 @@ __device__ inline uint32_t opt_rule(bool tcp, uint32_t t) {
         case 131: return 7u | 8u | 7u << 4;        // LooseSourceRoute
         default: return 0u;
     }
+}
+
+// The same rules computed in registers (no dependent LDS read per step): the kind index
+// by compares, then the length and the fixed flag from per-kind nibble / bit tables.
+#ifndef RPKT_OPT_RULE_ALU
+#define RPKT_OPT_RULE_ALU 0      // 1: opt_rule_alu in the paired walk instead of the LDS table
+#endif
+__device__ __forceinline__ uint32_t opt_rule_alu(bool tcp, uint32_t t) {
+    uint32_t k;
+    if (tcp) {
+        k = t == 2u ? 2u : t == 3u ? 3u : t == 4u ? 4u : t == 5u ? 5u : t == 8u ? 6u : t == 34u ? 7u : 0u;
+    } else {
+        k = t == 68u ? 2u : t == 7u ? 3u : t == 148u ? 4u : t == 134u ? 5u : t == 137u ? 6u
+          : t == 131u ? 7u : 0u;
+    }
+    // X per kind index 2..7 (nibble k) and fixed (bit k), as opt_rule's table
+    const uint32_t xs = tcp ? 0x2a223400u : 0x77643400u;
+    const uint32_t fx = tcp ? 0x5cu : 0xd0u;
+    const uint32_t x = (xs >> (4u * k)) & 15u;
+    return k == 0u ? 0u : (k | (((fx >> k) & 1u) << 3) | (x << 4));
 }
 
 // Both iterators' rule tables (IPv4: [0, 256), TCP: [256, 512)) into the block's LDS;
@@ -272,6 +295,151 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
 #pragma unroll
     for (int k = 0; k < 16; ++k) o[k] = 0;
     uint32_t ip_end = 0;
+#if RPKT_OPT_DEFER
+    // One branch-free step body: an EOL/NOP run or a TLV option, and the getters deferred:
+    // a step records only where the last option of its kind starts (a byte per kind,
+    // kinds 2..7: positions 0..3 in P0, 4..5 in P1), and the getters of both walks are
+    // read from LDS once, after the loop, at those positions.  The per-kind getter code
+    // inside the loop was a divergent branch tree executed every step.
+    uint32_t phase = S.tcp ? 0u : (ip_has ? 1u : 2u);
+    uint32_t at = phase == 0 ? slot_bias + S.t_lo : ip_at;
+    uint32_t base = at, end = at + (phase == 0 ? t_nb : ip_n);
+    uint32_t cnt = 0, kinds = 0, stop = RPKT_OPT_END, P0 = 0, P1 = 0, T0 = 0, T1 = 0;
+    uint64_t trace = 0;
+    uint32_t t_cnt = 0, t_kinds = 0, t_stop = 0, t_pos = 0;
+    uint64_t t_trace = 0;
+    while (phase < 2u) {
+        const bool tcp = phase == 0u;
+        if (at < end) {
+            const uint32_t a4 = at & ~3u;
+            const uint32_t d0 = align_bytes(lds32(win, a4 + 4u), lds32(win, a4), at & 3u);
+            const uint32_t t = d0 & 0xffu, hl = (d0 >> 8) & 0xffu;
+            const uint32_t nrem = end - at;
+            const uint32_t rule = rules[(tcp ? 256u : 0u) + t];
+            const bool run = t <= 1u;
+            const uint32_t x = d0 ^ (t ? 0x01010101u : 0u);
+            uint32_t kr = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u;
+            kr = kr < nrem ? kr : nrem;
+            const uint32_t X = rule >> 4, kind = rule & 7u;
+            const bool fixed = (rule & 8u) != 0u;
+            const bool ok = run | ((kind != 0u) & (nrem >= X) & (hl - X <= (fixed ? 0u : nrem - X)));
+            const uint32_t nn = run ? kr : 1u;                 // options this step yields
+            const uint32_t code = run ? t + 1u : kind + 1u;   // trace nibble
+            const uint32_t nibs = code * (0x1111u & ((1u << (4u * nn)) - 1u));
+            const uint32_t kb = run ? t : kind;
+            kinds |= ok ? 1u << kb : 0u;
+            trace |= (ok && cnt < 16u) ? (uint64_t)nibs << (4u * cnt) : 0ull;
+            // the TLV's start, as a byte at kind - 2 of P0 / P1 (kinds 2..7)
+            const uint32_t kp = kind - 2u, sh = 8u * (kp & 3u);
+            const bool rec = ok & !run;
+            const uint32_t v = (at - base) << sh, m = 0xffu << sh;
+            P0 = (rec && kp < 4u) ? (P0 & ~m) | v : P0;
+            P1 = (rec && kp >= 4u) ? (P1 & ~m) | v : P1;
+            cnt += ok ? nn : 0u;
+            stop = ok ? stop : (kind == 0u ? (uint32_t)RPKT_OPT_UNKNOWN : (uint32_t)RPKT_OPT_MALFORMED);
+            const uint32_t adv = run ? kr : (fixed ? X : hl);
+            end = ok ? end : at;
+            at = ok ? at + adv : at;
+        }
+        if (at >= end) {                                       // this walk ended
+            if (tcp) {
+                t_cnt = cnt, t_kinds = kinds, t_stop = stop, t_pos = at - base, t_trace = trace;
+                T0 = P0, T1 = P1;
+                phase = ip_has ? 1u : 2u;
+                base = at = ip_at;
+                end = ip_at + ip_n;
+                cnt = kinds = P0 = P1 = 0;
+                stop = RPKT_OPT_END;
+                trace = 0;
+            } else {
+                phase = 2u;
+            }
+        }
+    }
+    // the getters of the last option of each kind, from its recorded start: 12 bytes at
+    // `a` (the options read at most bytes a .. a + 9)
+    auto bytes12 = [&](uint32_t a, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
+        const uint32_t a4 = a & ~3u, sh = a & 3u;
+        const uint32_t R0 = lds32(win, a4), R1 = lds32(win, a4 + 4u);
+        const uint32_t R2 = lds32(win, a4 + 8u), R3 = lds32(win, a4 + 12u);
+        d0 = align_bytes(R1, R0, sh);
+        d1 = align_bytes(R2, R1, sh);
+        d2 = align_bytes(R3, R2, sh);
+    };
+    const uint32_t tb = slot_bias + S.t_lo;                    // TCP: this lane's frame
+    if (S.tcp) {
+        // word 0: tcp_count | tcp_stop << 8 | wscale << 16 | sack_blocks << 24;
+        // word 1: kinds | mss << 16; word 6: tcp_fo_len | tcp_end << 16
+        o[0] = t_cnt | (t_stop << 8);
+        o[1] = t_kinds;
+        o[6] = t_pos << 16;
+        o[12] = (uint32_t)t_trace;
+        o[13] = (uint32_t)(t_trace >> 32);
+    }
+    uint32_t d0, d1, d2;
+    if (__ballot(t_kinds & (1u << 2))) {                      // Mss
+        bytes12(tb + (T0 & 0xffu), d0, d1, d2);
+        if (t_kinds & (1u << 2)) o[1] |= be16_hi(d0) << 16;
+    }
+    if (__ballot(t_kinds & (1u << 3))) {                      // WindowScale
+        bytes12(tb + ((T0 >> 8) & 0xffu), d0, d1, d2);
+        if (t_kinds & (1u << 3)) o[0] |= ((d0 >> 16) & 0xffu) << 16;
+    }
+    if (__ballot(t_kinds & (1u << 5))) {                      // Sack
+        bytes12(tb + (T0 >> 24), d0, d1, d2);
+        if (t_kinds & (1u << 5)) {
+            const uint32_t h = (d0 >> 8) & 0xffu;
+            o[0] |= ((h - 2u) >> 3) << 24;
+            o[4] = h >= 6u ? bswap32(align_bytes(d1, d0, 2)) : 0u;
+            o[5] = h >= 10u ? bswap32(align_bytes(d2, d1, 2)) : 0u;
+        }
+    }
+    if (__ballot(t_kinds & (1u << 6))) {                      // Timestamp
+        bytes12(tb + (T1 & 0xffu), d0, d1, d2);
+        if (t_kinds & (1u << 6)) {
+            o[2] = bswap32(align_bytes(d1, d0, 2));
+            o[3] = bswap32(align_bytes(d2, d1, 2));
+        }
+    }
+    if (__ballot(t_kinds & (1u << 7))) {                      // FastOpen
+        bytes12(tb + ((T1 >> 8) & 0xffu), d0, d1, d2);
+        if (t_kinds & (1u << 7)) o[6] |= (d0 >> 8) & 0xffu;
+    }
+    if (ip_has) {
+        // word 7: ip_count | ip_stop << 8 | ip_kinds << 16; ip_end: byte 27
+        ip_end = at - base;
+        o[7] = cnt | (stop << 8) | (kinds << 16);
+        o[14] = (uint32_t)trace;
+        o[15] = (uint32_t)(trace >> 32);
+    }
+    const uint32_t ib = ip_at;                                 // IPv4: the partner frame
+    if (__ballot(kinds & (1u << 2))) {                        // Timestamp
+        bytes12(ib + (P0 & 0xffu), d0, d1, d2);
+        if (kinds & (1u << 2)) o[9] = d0 >> 8;
+    }
+    if (__ballot(kinds & (1u << 3))) {                        // RecordRoute
+        bytes12(ib + ((P0 >> 8) & 0xffu), d0, d1, d2);
+        if (kinds & (1u << 3)) o[8] = (d0 >> 8) << 16;
+    }
+    if (__ballot(kinds & (1u << 4))) {                        // RouteAlert
+        bytes12(ib + ((P0 >> 16) & 0xffu), d0, d1, d2);
+        if (kinds & (1u << 4)) o[8] |= be16_hi(d0);
+    }
+    if (__ballot(kinds & (1u << 5))) {                        // CommercialSecurity
+        bytes12(ib + (P0 >> 24), d0, d1, d2);
+        if (kinds & (1u << 5)) o[11] = bswap32(align_bytes(d1, d0, 2));
+    }
+    if (__ballot(kinds & (3u << 6))) {                        // Strict / LooseSourceRoute
+        // both kinds set the same getters: the later of the two options wins
+        const uint32_t p6 = P1 & 0xffu, p7 = (P1 >> 8) & 0xffu;
+        const uint32_t ps = !(kinds & (1u << 6)) ? p7 : (!(kinds & (1u << 7)) ? p6 : max(p6, p7));
+        bytes12(ib + ps, d0, d1, d2);
+        if (kinds & (3u << 6)) {
+            o[9] |= ((d0 >> 16) & 0xffu) << 24;
+            o[10] = bswap32(align_bytes(d1, d0, 3));
+        }
+    }
+#else
     // phase 0: this frame's TCP walk; 1: frame q's IPv4 walk; 2: done
     uint32_t phase = S.tcp ? 0u : (ip_has ? 1u : 2u);
     OptCur c;
@@ -299,7 +467,8 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
                 c.cnt += k;
                 c.at += k;
             } else {
-                const uint32_t rule = rules[(tcp ? 256u : 0u) + t];
+                const uint32_t rule = RPKT_OPT_RULE_ALU ? opt_rule_alu(tcp, t)
+                                                        : rules[(tcp ? 256u : 0u) + t];
                 const uint32_t hl = (d0 >> 8) & 0xffu;     // n >= 2 whenever a rule can pass
                 const uint32_t X = rule >> 4, kind = rule & 7u;
                 const bool fixed = (rule & 8u) != 0u;
@@ -363,6 +532,7 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
             }
         }
     }
+#endif  // RPKT_OPT_DEFER
     // rows: this frame's TCP words, then frame q's IPv4 words (word 6's top byte last)
     wave_sync();                                               // every walk has ended
     uint32_t* st = reinterpret_cast<uint32_t*>(win);

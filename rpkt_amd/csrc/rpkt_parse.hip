@@ -970,8 +970,9 @@ int parse_options(const rpkt_batch_t* b, uint32_t flags, void* recs_dev, rpkt_op
 // rpkt_amd/build.py), whose only entry point is the hidden
 // rpkt_gpu_parse_batch_compact_w64 the first compile hands strided batches of short
 // frames to: every frame lies inside its 64-B window (parse_w64_fits), so the headers
-// and the L4 bytes are all in LDS, a wave's LDS drops from 9.7 to 5.6 KB, and with the
-// 16-B records kept in registers the VGPRs, not the LDS, set the waves per SIMD.
+// and the L4 bytes are all in LDS, a wave's LDS drops from 9.7 to 6.5 KB (the window
+// area keeps the 64 x 21-dword record stage's 5376 B), and with the 16-B records kept in
+// registers the VGPRs, not the LDS, set the waves per SIMD.
 #ifndef RPKT_PARSE_W64_ON
 #define RPKT_PARSE_W64_ON 1
 #endif

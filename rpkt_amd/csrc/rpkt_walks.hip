@@ -840,7 +840,8 @@ int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void
 }
 
 #ifdef RPKT_ABLATE
-// Development hook (librpkt_gpu_ablate.so only: the walk with F frames per lane
+// Development hook (librpkt_gpu_ablate.so only, not part of include/rpkt_gpu.h): the walk
+// with F frames per lane
 // (1, 2, 4, 8), for timing the choice of kLayFrames.  (Tried and dropped, DESIGN.md:
 // prefetching a lane's next frame window into registers, 84 -> 90 us; per-group steps
 // specialised at compile time and run one uniform group after another, 84 -> 195 us
