@@ -96,7 +96,7 @@ def test_layers_frames_per_lane_variants(torch):
     """The walk with 1, 2, 4 and 8 frames per lane (development hook behind
     tools/ablate_layers.py) gives the product kernel's records byte for byte."""
     import ctypes
-    L = engine.lib()
+    L = engine.ablate_lib()          # the variants are development hooks
     L.rpkt_gpu_debug_layers_variant.argtypes = [ctypes.POINTER(engine.Batch), ctypes.c_void_p,
                                                 ctypes.c_int, ctypes.c_void_p]
     L.rpkt_gpu_debug_layers_variant.restype = ctypes.c_int
