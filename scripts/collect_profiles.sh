@@ -6,7 +6,7 @@ set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
 RND=${RND:-r02}
-for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact walks build3 optsc5}; do
+for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact c5_opts c5_opts_compact walks build3 optsc5}; do
     P=$G/prof_$t; D=$R/profiles/${RND}_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
@@ -18,8 +18,8 @@ for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact walks build3 optsc5}; do
         python3 "$R/tools/traffic.py" "$P" tx:$t "$R/profiles/traffic_tx.json"
     elif [ "$t" = walks ]; then
         python3 "$R/tools/traffic.py" "$P" tx "$R/profiles/traffic_tx.json"
-    elif [ "${t%_compact}" != "$t" ]; then
-        c=${t#c}; python3 "$R/tools/traffic.py" "$P" "${c%_compact}" "$R/profiles/traffic_$t.json"
+    elif [ "${t%_compact}" != "$t" ] || [ "${t%_opts}" != "$t" ]; then
+        c=${t#c}; python3 "$R/tools/traffic.py" "$P" "${c%%_*}" "$R/profiles/traffic_$t.json"
     else
         python3 "$R/tools/traffic.py" "$P" "${t#c}" "$R/profiles/traffic_$t.json"
     fi
