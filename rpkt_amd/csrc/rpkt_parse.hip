@@ -1159,7 +1159,8 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         case 16: case 17: case 18: case 19: {
             const uint32_t in16 = (uint32_t)(b->frames_bytes / 16);
             const uint32_t out16 = variant >= 18 ? in16 : b->n * (RPKT_REC_BYTES / 16);
-            const dim3 g(1024), blk(kWave * kWavesPerBlock);     // 4096 waves: one per SIMD slot
+            // 16384 waves: tools/copybw.hip's best mixed shape (4096 waves: 5.1-5.4 TB/s)
+            const dim3 g(4096), blk(kWave * kWavesPerBlock);
             switch (variant) {
                 case 16: return launch(wave_stream_ref_kernel<0, false, false>, g, blk, 0, st,
                                        b->frames_dev, in16, (u32x4*)recs, out16);
