@@ -4,6 +4,9 @@
 #include "rpkt_opts.h"
 #include "rpkt_proto_table.h"
 
+#include <map>
+#include <mutex>
+
 namespace {
 
 // ---- option iterators: TcpOptionsIter / Ipv4OptionsIter over a parsed batch ----
@@ -151,10 +154,29 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 // in), then the next header's first 20 bytes.  Rarer needs (members past the second,
 // the byte-keyed lookup groups, a member other than the first) are read under
 // wave-uniform branches, taken only by waves that have a lane needing them.
-constexpr int kLayChunks = 8;                  // 128 B slot from a 16-B boundary
-constexpr int kLaySlot = 132;                  // 33 dwords: conflict-free lanes
+#ifndef RPKT_LAY_CHUNKS
+#define RPKT_LAY_CHUNKS 8
+#endif
+// Development switches (same-process A/B in DESIGN.md, layers_kernel; all off in the
+// product build)
+#ifndef RPKT_LAY_STAGE_REC
+#define RPKT_LAY_STAGE_REC 0     // 1: records stored through the slots, 64 B per 4 lanes
+#endif
+#ifndef RPKT_LAY_COOP_FILL
+#define RPKT_LAY_COOP_FILL 0     // 1: ... and the new frames' windows loaded cooperatively
+#endif
+#ifndef RPKT_LAY_STAGE_MIN
+#define RPKT_LAY_STAGE_MIN 16    // ... when at least this many walks of the wave end together
+#endif
+
+constexpr int kLayChunks = RPKT_LAY_CHUNKS;    // 128 B slot from a 16-B boundary
+constexpr int kLaySlot = 16 * kLayChunks + 4;  // 33 dwords: conflict-free lanes
+static_assert((kLaySlot / 4) % 2 == 1, "odd dword stride");
 struct LayScratch {
     uint8_t win[kWave * kLaySlot];             // 8448 B
+#if RPKT_LAY_STAGE_REC
+    uint32_t emap[kWave];                      // lanes whose walk ended, by rank
+#endif
 };
 
 struct LayerWin {
@@ -599,6 +621,9 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
 // taking the next untaken frame when its walk ends (82.9 -> 68.7 us on the capture
 // mix vs four fixed frames per lane, profiles/r02_fwd/ablate_layers_c9.log)
 constexpr int kLayFrames = 4;
+#ifndef RPKT_LAY_RUNTIME_POOL
+#define RPKT_LAY_RUNTIME_POOL 0  // 1: block pools sized for one round of resident blocks
+#endif
 // A lane stores its 64-B record as four 16-B stores when its walk ends, so every store
 // instruction writes 16 B into each of up to 64 different records: with the default
 // policy L2 merges a record's four pieces into one line write, non-temporal stores do not
@@ -611,11 +636,14 @@ constexpr int kLayFrames = 4;
 #define RPKT_LAY_BLOCK_POOL 1    // 0: one pool per wave
 #endif
 
-template <int F, bool DYN = false>
+// ABL (librpkt_gpu_ablate.so timing only, results not meaningful), bits: 1 = a taken
+// frame walks the slot's stale bytes (no refill), 2 = no record stores, 4 = every walk
+// ends after its Ethernet step
+template <int F, bool DYN = false, int ABL = 0>
 __global__ __launch_bounds__(kWave * kWavesPerBlock)
 void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
-                   uint32_t n, rpkt_layers_t* __restrict__ out) {
+                   uint32_t n, rpkt_layers_t* __restrict__ out, uint32_t pool) {
     __shared__ __attribute__((aligned(16))) LayScratch scratch[kWavesPerBlock];
     // the protocol table in LDS: lanes walk different protocols, so table reads are
     // per-lane (divergent) loads; from LDS they cost tens of cycles instead of a
@@ -632,7 +660,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
     LayScratch& W = scratch[wid];
-    const uint32_t bb = blockIdx.x * kWavesPerBlock * (kWave * F);   // the block's frames
+    const uint32_t bb = blockIdx.x * pool;                   // the block's frames (kBlk)
     const uint32_t p0 = kBlk ? bb + wid * kWave : (blockIdx.x * kWavesPerBlock + wid) * (kWave * F);
     if (p0 >= n) return;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
@@ -690,6 +718,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     uint32_t pend = 0;
     if constexpr (kEth) {
         if (active) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
+        if constexpr ((ABL & 4) != 0) pend = active ? (uint32_t)RPKT_L_END : 0u;
     }
     while (__ballot(active)) {
         uint32_t stop = pend;
@@ -742,23 +771,107 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 if (lane == 0) b0 = atomicAdd(&blk_taken, (uint32_t)__builtin_popcountll(sm));
                 kbase = (uint32_t)__shfl((int)b0, 0, kWave);
             }
-            if (stop) {
-                u32x4* dst = reinterpret_cast<u32x4*>(out + i);
+            // Records of the ended walks.  When many walks end together (a uniform
+            // batch) they go through their (now free) slots, so that four neighbouring
+            // lanes store one record's four 16-B pieces (whole 64-B writes instead of
+            // 16-B pieces of 64 records per store instruction); a few at a time are
+            // stored by their own lanes.
+            const uint32_t m = (uint32_t)__builtin_popcountll(sm);
+            const bool staged = RPKT_LAY_STAGE_REC && m >= (uint32_t)RPKT_LAY_STAGE_MIN;
+            bool filled = false;
+            Frame fq{0u, 0u};
+#if RPKT_LAY_STAGE_REC
+            if (staged) {
+                if (stop) {
+                    uint32_t* r = reinterpret_cast<uint32_t*>(Wn.base);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-#if RPKT_LAY_REC_NT
-                    __builtin_nontemporal_store(u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]},
-                                                &dst[k]);
-#else
-                    dst[k] = u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+                    for (int k = 0; k < 16; ++k) r[k] = o[k];
+                    W.emap[rank] = (uint32_t)lane;
+                }
+                wave_sync();
+                if constexpr ((ABL & 2) == 0) {
+                    for (uint32_t q0 = 0; q0 < m; q0 += kWave / 4) {   // wave-uniform
+                        const uint32_t q = q0 + (uint32_t)(lane >> 2), j = (uint32_t)lane & 3u;
+                        const uint32_t src = W.emap[q < m ? q : m - 1u];
+                        const uint32_t isrc =
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)i);
+                        const uint32_t* pr =
+                            reinterpret_cast<const uint32_t*>(&W.win[src * kLaySlot]) + 4u * j;
+                        const u32x4 v{pr[0], pr[1], pr[2], pr[3]};
+                        if (q < m) reinterpret_cast<u32x4*>(out + isrc)[j] = v;
+                    }
+                }
+                wave_sync();
+            }
+            // DYN block pools, many walks ended: the new frames (ranks 0..m-1 take frames
+            // kbase + rank, consecutive) have their windows loaded cooperatively, each
+            // load instruction covering whole windows of 64 / kLayChunks frames, as the
+            // first tiles are; the lanes' own refill is skipped
+            if constexpr (DYN && kBlk && RPKT_LAY_COOP_FILL && (ABL & 1) == 0) {
+                if (staged) {
+                    const uint32_t kq = kbase + (uint32_t)lane, iq = bb + kq;
+                    if ((uint32_t)lane < m && kq < pool && iq < n) fq = spans.get(iq);
+                    u32x4 d[kLayChunks];
+                    uint32_t addr[kLayChunks];
+                    uint32_t fix = 0;
+#pragma unroll
+                    for (int k = 0; k < kLayChunks; ++k) {
+                        const int c = k * kWave + lane;
+                        const int q = c / kLayChunks, j = c % kLayChunks;
+                        const uint32_t qo = (uint32_t)__shfl((int)fq.off, q, kWave);
+                        const uint32_t ql = (uint32_t)__shfl((int)fq.len, q, kWave);
+                        const uint32_t a = (qo & ~15u) + 16u * j;
+                        addr[k] = ((uint32_t)q < m && a < qo + ql) ? a : fb;
+                        fix |= (uint32_t)straddles(addr[k], fb) << k;
+                    }
+#pragma unroll
+                    for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+#pragma unroll
+                    for (int k = 0; k < kLayChunks; ++k) {
+                        const int c = k * kWave + lane;
+                        const uint32_t q = (uint32_t)(c / kLayChunks);
+                        u32x4 v = d[k];
+                        if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+                        if (q < m) {
+                            uint32_t* dst = reinterpret_cast<uint32_t*>(
+                                &W.win[W.emap[q] * kLaySlot + (c % kLayChunks) * 16]);
+                            dst[0] = v.x;
+                            dst[1] = v.y;
+                            dst[2] = v.z;
+                            dst[3] = v.w;
+                        }
+                    }
+                    wave_sync();
+                    filled = true;
+                    // each taking lane's frame from the lane of its rank (full EXEC here)
+                    fq.off = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rank << 2), (int)fq.off);
+                    fq.len = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(rank << 2), (int)fq.len);
+                }
+            }
 #endif
+            if (stop) {
+                if (!staged) {
+                    u32x4* dst = reinterpret_cast<u32x4*>(out + i);
+#pragma unroll
+                    for (int k = 0; k < ((ABL & 2) ? 0 : 4); ++k) {
+#if RPKT_LAY_REC_NT
+                        __builtin_nontemporal_store(
+                            u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, &dst[k]);
+#else
+                        dst[k] = u32x4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+#endif
+                    }
                 }
                 Frame f = fr[0];
                 if constexpr (DYN) {
                     const uint32_t k = kbase + rank;
                     i = (kBlk ? bb : p0) + k;
-                    active = k < (uint32_t)(kWave * F * (kBlk ? kWavesPerBlock : 1)) && i < n;
-                    if (active) f = spans.get(i);
+                    active = k < (kBlk ? pool : (uint32_t)(kWave * F)) && i < n;
+                    if (filled) {
+                        f = fq;                               // this rank's, from its lane
+                    } else if (active) {
+                        f = spans.get(i);
+                    }
                 } else {
                     fk += 1;
                     i += kWave;
@@ -772,9 +885,18 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 Wn.off = f.off;
                 pend = 0;
                 if (active) {
-                    Wn.refill(0u);
+                    if constexpr ((ABL & 1) != 0) {
+                        Wn.bias = f.off & 15u;
+                        Wn.avail = (uint32_t)(kLayChunks * 16) - Wn.bias;
+                    } else if (filled) {
+                        Wn.bias = f.off & 15u;
+                        Wn.avail = (uint32_t)(kLayChunks * 16) - Wn.bias;
+                    } else {
+                        Wn.refill(0u);
+                    }
                     if constexpr (kEth) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
                     else H = lay_hdr(Wn, 0u, false);
+                    if constexpr ((ABL & 4) != 0) pend = (uint32_t)RPKT_L_END;
                 }
             }
             if constexpr (DYN) taken += (uint32_t)__builtin_popcountll(sm);
@@ -782,14 +904,52 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
 }
 
-template <int F, bool DYN = false>
+// Blocks of kernel k resident on the current device at once (CUs x blocks per CU),
+// once per device and kernel.
+int resident_blocks(const void* k, uint32_t block_threads, uint32_t& out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, uint32_t> cache;
+    int dev = 0;
+    int rc = hip_check(hipGetDevice(&dev));
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({dev, k});
+    if (it != cache.end()) {
+        out = it->second;
+        return RPKT_OK;
+    }
+    int cus = 0, per_cu = 0;
+    rc = hip_check(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (rc) return rc;
+    rc = hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, (int)block_threads, 0));
+    if (rc) return rc;
+    out = (uint32_t)(cus > 0 ? cus : 1) * (uint32_t)(per_cu > 0 ? per_cu : 1);
+    cache[{dev, k}] = out;
+    return RPKT_OK;
+}
+
+// F = 0: the block pools are sized at run time so that the grid is one round of
+// resident blocks (each block walks ceil(n / resident) frames, at least its waves'
+// first tiles); F > 0: pools of 64 F frames per wave (kLayFrames, the ablations).
+template <int F, bool DYN = false, int ABL = 0>
 int launch_layers(const rpkt_batch_t* b, uint32_t flen, rpkt_layers_t* layers_dev, void* stream) {
     const uint32_t per_block = kWave * kWavesPerBlock;
-    const uint32_t waves = (uint32_t)((b->n + (uint64_t)kWave * F - 1) / ((uint64_t)kWave * F));
-    const uint32_t grid = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    return launch(layers_kernel<F, DYN>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
+    uint32_t pool = per_block * (F > 0 ? F : 1), grid;
+    if constexpr (F == 0) {
+        static_assert(DYN, "run-time pools are block pools");
+        uint32_t res = 0;
+        const int rc = resident_blocks((const void*)layers_kernel<F, DYN, ABL>, per_block, res);
+        if (rc) return rc;
+        const uint32_t want = (uint32_t)(((uint64_t)b->n + res - 1) / res);
+        pool = want > per_block ? want : per_block;
+        grid = (uint32_t)(((uint64_t)b->n + pool - 1) / pool);
+    } else {
+        const uint32_t waves = (uint32_t)((b->n + (uint64_t)kWave * F - 1) / ((uint64_t)kWave * F));
+        grid = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    }
+    return launch(layers_kernel<F, DYN, ABL>, dim3(grid), dim3(per_block), 0, (hipStream_t)stream,
                   b->frames_dev, (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n,
-                  layers_dev);
+                  layers_dev, pool);
 }
 
 }  // namespace
@@ -836,7 +996,11 @@ int rpkt_gpu_layers_batch(const rpkt_batch_t* b, rpkt_layers_t* layers_dev, void
     if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
     if (((uintptr_t)layers_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+#if RPKT_LAY_RUNTIME_POOL
+    return launch_layers<0, true>(b, flen, layers_dev, stream);
+#else
     return launch_layers<kLayFrames, true>(b, flen, layers_dev, stream);
+#endif
 }
 
 #ifdef RPKT_ABLATE
@@ -860,6 +1024,14 @@ int rpkt_gpu_debug_layers_variant(const rpkt_batch_t* b, rpkt_layers_t* layers_d
         case 104: return launch_layers<4, true>(b, flen, layers_dev, stream);   // pooled
         case 102: return launch_layers<2, true>(b, flen, layers_dev, stream);
         case 108: return launch_layers<8, true>(b, flen, layers_dev, stream);
+        case 201: return launch_layers<4, true, 1>(b, flen, layers_dev, stream);  // ablations
+        case 202: return launch_layers<4, true, 2>(b, flen, layers_dev, stream);
+        case 203: return launch_layers<4, true, 3>(b, flen, layers_dev, stream);
+        case 204: return launch_layers<4, true, 4>(b, flen, layers_dev, stream);
+        case 205: return launch_layers<4, true, 5>(b, flen, layers_dev, stream);
+        case 206: return launch_layers<4, true, 6>(b, flen, layers_dev, stream);
+        case 207: return launch_layers<4, true, 7>(b, flen, layers_dev, stream);
+        case 300: return launch_layers<0, true>(b, flen, layers_dev, stream);     // run-time pools
         default: return RPKT_E_INVAL;
     }
 }

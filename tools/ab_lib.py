@@ -33,7 +33,7 @@ def build_b(out_dir, extra):
         objs.append(o)
     lib = os.path.join(out_dir, "librpkt_gpu.so")
     subprocess.check_call([build.HIPCC, "--offload-arch=" + build.ARCH, "-shared", "-fPIC",
-                           "-o", lib] + objs + ["-L" + build.ROCM_LIB, "-lrccl"])
+                           "-o", lib] + objs + ["-ldl"])
     print(lib)
 
 
