@@ -213,6 +213,35 @@ def time_parse(dbs, recs, flags, steps, warmup, world, flow=None, min_warm_s=0.3
     return wall, kern_ms, warm_launches
 
 
+def fused_vs_parse(dbs, recs, obufs, flags, compact, rounds=7, k=10):
+    """The fused pass against the parse alone on the same batches, timed interleaved
+    (k launches of each per round, HIP events on the launch stream; medians): the
+    ratio does not move with the box's clocks as two legs timed minutes apart do."""
+    stream = torch.cuda.current_stream()
+    R = len(dbs)
+    parse = engine.parse_batch_compact if compact else engine.parse_batch
+    legs = {
+        "parse": lambda j: parse(dbs[j % R], flags, recs=recs[j % R], stream=stream),
+        "fused": lambda j: engine.parse_options_batch(dbs[j % R], flags, recs=recs[j % R],
+                                                      opts=obufs[j % R], stream=stream,
+                                                      compact=compact),
+    }
+    t = {name: [] for name in legs}
+    for r in range(rounds + 1):                     # round 0 warms both
+        for name, fn in legs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for j in range(k):
+                fn(j)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            if r:
+                t[name].append(e0.elapsed_time(e1) / k)
+    med = {name: sorted(v)[len(v) // 2] for name, v in t.items()}
+    return {"parse_kernel_ms": round(med["parse"], 5), "fused_kernel_ms": round(med["fused"], 5),
+            "ratio": round(med["fused"] / med["parse"], 4), "rounds": rounds, "launches": k}
+
+
 def pmc_traffic(cfg, compact=False, opts=False):
     """Per-launch HBM traffic of parse_kernel for this config (and record size, and the
     fused option walks) from the rocprofv3 PMC summary committed under profiles/
@@ -484,6 +513,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         out["what"] = ("rpkt_gpu_parse_options_batch%s: the parse + sums and both option walks "
                        "(Ipv4OptionsIter, TcpOptionsIter) in one pass, 64-B rpkt_opts_t per frame"
                        % ("_compact" if compact else ""))
+        out["vs_parse_same_run"] = fused_vs_parse(dbs, recs, obufs, flags, compact)
     if cfg == 4:
         torch.cuda.synchronize()
         barrier(world)
