@@ -62,6 +62,25 @@ def test_library_loads_without_rccl(L):
     assert isinstance(L.rpkt_gpu_coll_version(), int)
 
 
+def test_collective_binds_torchs_rccl(L):
+    """Under PyTorch the engine's RCCL calls bind the copy torch already loaded (whose
+    ProcessGroupNCCL owns the communicator handed to rpkt_gpu_flow_reduce): same version,
+    and no second librccl mapped into the process."""
+    import subprocess
+    import sys
+    code = (
+        "import torch, ctypes\n"
+        "from rpkt_amd import engine\n"
+        "v = engine.lib().rpkt_gpu_coll_version()\n"
+        "a, b, c = torch.cuda.nccl.version()\n"
+        "maps = {l.split()[-1] for l in open('/proc/self/maps').read().splitlines() if 'rccl' in l}\n"
+        "print(v, a * 10000 + b * 100 + c, len(maps))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT,
+                         timeout=600, check=True).stdout.split()
+    v, tv, copies = (int(x) for x in out[-3:])
+    assert v == tv and copies == 1
+
+
 def test_abi_version_and_info(L):
     assert L.rpkt_gpu_abi_version() == 1
     assert b"gfx950" in L.rpkt_gpu_build_info()
