@@ -581,6 +581,54 @@ def run_host(args):
     return out
 
 
+def run_rx_graph(args):
+    """A receive loop of small batches (rpkt_amd.graphs): a ring of `slots` batches of
+    config-2 frames; per pass, each slot's parse with flow events and one flow count of
+    the pass's events.  Timed as eager engine calls from Python (each through ctypes) and
+    as one captured hipGraph replayed per pass, with the parses on the current stream or
+    forked over 4 streams.  Every mode must leave identical counters."""
+    from rpkt_amd import graphs
+    out = {}
+    nb = 1024
+    for spec in [x for x in args.rx_graph.split(",") if x.strip()]:
+        n, slots = (int(v) for v in spec.split("x"))
+        hb = gen.make_batch(2, n, seed=gen.DEFAULT_SEED[2])
+        ring = graphs.batch_ring(hb, slots)
+        recs = [engine.alloc_records(n) for _ in range(slots)]
+        ev_all = torch.empty(n * slots, dtype=torch.int64, device="cuda")
+        ws = engine.flow_workspace(n * slots, nb)
+        side = [torch.cuda.Stream() for _ in range(4)]
+        res, cnts = {}, []
+        for mode in ("eager", "graph", "eager_4streams", "graph_4streams"):
+            cnt = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
+            cnts.append(cnt)
+            streams = side if mode.endswith("4streams") else None
+            fn = (lambda cnt=cnt, streams=streams:
+                  graphs.rx_pass(ring, recs, ev_all, cnt, ws, gen.FLAGS[2], nb, streams))
+            step = fn
+            if mode.startswith("graph"):
+                step = graphs.CapturedLoop(fn).replay      # runs one warm pass, then captures
+            else:
+                fn()                                       # the same warm pass
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            res[mode] = {"mpps": n * slots * args.steps / dt / 1e6,
+                         "us_per_pass": dt / args.steps * 1e6}
+        res["counters_identical"] = all(torch.equal(cnts[0], c) for c in cnts[1:])
+        out["%dx%d" % (n, slots)] = {
+            k: ({kk: round(vv, 3) for kk, vv in v.items()} if isinstance(v, dict) else v)
+            for k, v in res.items()}
+        del ring, recs, ev_all
+        torch.cuda.empty_cache()
+    return out
+
+
 def copy_ceiling(dbs, recs, steps):
     """Measured device-to-device copy ceilings beside config 2, same
     stream and event timing as the parse (development library's streaming references):
@@ -818,6 +866,9 @@ def main():
     ap.add_argument("--host", default="2,3",
                     help="configs also timed host-inclusive at N=1 (pinned H2D frames -> parse "
                          "-> D2H records, rpkt_amd.pipeline): extra.host_inclusive")
+    ap.add_argument("--rx-graph", default="16384x64,65536x16",
+                    help="receive loops of small config-2 batches, FRAMESxSLOTS, timed eager "
+                         "and as a replayed hipGraph at N=1 (rpkt_amd.graphs): extra.rx_graph")
     ap.add_argument("--strong", default="2,3",
                     help="configs also timed as one batch split over the ranks "
                          "(extra.config<N>_strong)")
@@ -881,6 +932,8 @@ def main():
                                                         opts=True)
     if world == 1 and args.host.strip():
         extra["host_inclusive"] = run_host(args)
+    if world == 1 and args.rx_graph.strip():
+        extra["rx_graph"] = run_rx_graph(args)
     if want_cpu and not args.no_config1:
         extra["config1"] = run_config1(args)
 

@@ -109,7 +109,7 @@ def build_gen(force=False):
     return GEN_LIB
 
 
-EXAMPLES = ("parse_batch", "flow_reduce")
+EXAMPLES = ("parse_batch", "flow_reduce", "rx_graph")
 EXAMPLE_BIN = os.path.join(ROOT, "examples", "parse_batch")
 FLOW_REDUCE_BIN = os.path.join(ROOT, "examples", "flow_reduce")
 
