@@ -585,8 +585,9 @@ def run_rx_graph(args):
     """A receive loop of small batches (rpkt_amd.graphs): a ring of `slots` batches of
     config-2 frames; per pass, each slot's parse with flow events and one flow count of
     the pass's events.  Timed as eager engine calls from Python (each through ctypes) and
-    as one captured hipGraph replayed per pass, with the parses on the current stream or
-    forked over 4 streams.  Every mode must leave identical counters."""
+    as one captured hipGraph replayed per pass, with the parses on the current stream,
+    forked over 4 streams, or all slots in one rpkt_gpu_parse_ring call.  Every mode must
+    leave identical counters."""
     from rpkt_amd import graphs
     out = {}
     nb = 1024
@@ -598,15 +599,20 @@ def run_rx_graph(args):
         ev_all = torch.empty(n * slots, dtype=torch.int64, device="cuda")
         ws = engine.flow_workspace(n * slots, nb)
         side = [torch.cuda.Stream() for _ in range(4)]
+        rslots = engine.ring_slots(ring, recs, [ev_all[k * n:(k + 1) * n] for k in range(slots)])
         res, cnts = {}, []
-        for mode in ("eager", "graph", "eager_4streams", "graph_4streams"):
+        for mode in ("eager", "graph", "eager_4streams", "graph_4streams", "ring", "ring_graph"):
             cnt = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
             cnts.append(cnt)
             streams = side if mode.endswith("4streams") else None
-            fn = (lambda cnt=cnt, streams=streams:
-                  graphs.rx_pass(ring, recs, ev_all, cnt, ws, gen.FLAGS[2], nb, streams))
+            if mode.startswith("ring"):
+                fn = (lambda cnt=cnt: graphs.rx_pass_ring(rslots, ev_all, n * slots, cnt, ws,
+                                                          gen.FLAGS[2], nb))
+            else:
+                fn = (lambda cnt=cnt, streams=streams:
+                      graphs.rx_pass(ring, recs, ev_all, cnt, ws, gen.FLAGS[2], nb, streams))
             step = fn
-            if mode.startswith("graph"):
+            if mode.startswith("graph") or mode == "ring_graph":
                 step = graphs.CapturedLoop(fn).replay      # runs one warm pass, then captures
             else:
                 fn()                                       # the same warm pass

@@ -130,6 +130,17 @@ pub struct rpkt_batch_t {
     pub reserved: u32,
 }
 
+/// One slot of a receive ring (rpkt_gpu_parse_ring): a batch, its records and (with
+/// RPKT_F_FLOW_EV) its flow events.
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct rpkt_ring_slot_t {
+    pub batch: rpkt_batch_t,
+    pub recs_dev: *mut rpkt_rec_t,
+    pub flow_ev_dev: *mut rpkt_flow_ev_t,
+}
+pub const RPKT_RING_MAX_SLOTS: u32 = 32;
+
 #[repr(C)]
 #[derive(Clone, Copy, Debug)]
 pub struct rpkt_chains_t {
@@ -228,6 +239,10 @@ extern "C" {
                                         recs_dev: *mut rpkt_rec16_t,
                                         flow_ev_dev: *mut rpkt_flow_ev_t, n_buckets: u32,
                                         stream: *mut c_void) -> c_int;
+
+    /// Every slot parsed as by rpkt_gpu_parse_batch, RPKT_RING_MAX_SLOTS slots per launch.
+    pub fn rpkt_gpu_parse_ring(slots: *const rpkt_ring_slot_t, n_slots: u32, flags: u32,
+                               n_buckets: u32, stream: *mut c_void) -> c_int;
 
     pub fn rpkt_gpu_flow_workspace_bytes(n: u32, n_buckets: u32) -> usize;
     pub fn rpkt_gpu_flow_count(flow_ev_dev: *const rpkt_flow_ev_t, n: u32, n_buckets: u32,

@@ -66,10 +66,17 @@ struct Fork {                    // side streams and their fork / join events
     std::vector<hipEvent_t> join;
 };
 
-// one pass of the loop on stream st: the slots' parses (over the side streams when there
+// one pass of the loop on stream st: the slots' parses (one rpkt_gpu_parse_ring call when
+// `rs` is given, else one rpkt_gpu_parse_batch per slot, over the side streams when there
 // are any), then the pass's flow counters
 static int pass(std::vector<Slot>& ring, rpkt_flow_ev_t* ev_all, uint32_t n_ev, uint64_t* counters,
-                void* ws, uint32_t nb, hipStream_t st, Fork& F) {
+                void* ws, uint32_t nb, hipStream_t st, Fork& F,
+                const std::vector<rpkt_ring_slot_t>* rs) {
+    if (rs) {
+        const int rc = rpkt_gpu_parse_ring(rs->data(), (uint32_t)rs->size(),
+                                           RPKT_F_IP_SUM | RPKT_F_FLOW_EV, nb, st);
+        return rc ? rc : rpkt_gpu_flow_count(ev_all, n_ev, nb, counters, ws, st);
+    }
     const size_t S = F.side.size();
     if (S) {
         if (hipEventRecord(F.fork, st) != hipSuccess) return RPKT_E_HIP;
@@ -132,14 +139,20 @@ int main(int argc, char** argv) {
     printf("ring: %u slots x %u frames x 64 B; per pass %u parses + one flow count of %u events\n",
            slots, n, slots, n_ev);
 
+    std::vector<rpkt_ring_slot_t> rs(slots);
+    for (uint32_t q = 0; q < slots; q++) rs[q] = rpkt_ring_slot_t{ring[q].b, ring[q].recs, ring[q].ev};
+
     std::vector<uint64_t> c_ref, c_got((size_t)(nb + 1) * 4);
     std::vector<rpkt_rec_t> r_ref, r_got((size_t)n);
     bool same = true;
     const double frames = (double)n_ev * reps;
-    for (int mode = 0; mode < 4; mode++) {           // eager / graph x 1 / `streams` streams
+    // eager / graph x {one stream, `streams` streams, the ring call}
+    for (int mode = 0; mode < 6; mode++) {
         const bool graph = mode & 1;
-        Fork& F = mode & 2 ? many : one;
-        if ((mode & 2) && F.side.empty()) continue;
+        const int how = mode >> 1;                    // 0: one stream, 1: forked, 2: ring
+        Fork& F = how == 1 ? many : one;
+        if (how == 1 && F.side.empty()) continue;
+        const std::vector<rpkt_ring_slot_t>* R = how == 2 ? &rs : nullptr;
         CK(hipMemset(counters, 0, cbytes));
         CK(hipMemset(ring[slots - 1].recs, 0, (size_t)n * sizeof(rpkt_rec_t)));
         hipGraph_t g = nullptr;
@@ -147,7 +160,7 @@ int main(int argc, char** argv) {
         size_t nodes = 0;
         if (graph) {
             CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-            const int rc_cap = pass(ring, ev_all, n_ev, counters, ws, nb, st, F);
+            const int rc_cap = pass(ring, ev_all, n_ev, counters, ws, nb, st, F, R);
             CK(hipStreamEndCapture(st, &g));
             RC(rc_cap);
             CK(hipGraphGetNodes(g, nullptr, &nodes));
@@ -155,7 +168,7 @@ int main(int argc, char** argv) {
         }
         auto run = [&]() -> int {
             if (graph) return hipGraphLaunch(ge, st) == hipSuccess ? RPKT_OK : RPKT_E_HIP;
-            return pass(ring, ev_all, n_ev, counters, ws, nb, st, F);
+            return pass(ring, ev_all, n_ev, counters, ws, nb, st, F, R);
         };
         RC(run());                                     // the warm pass
         CK(hipEventRecord(e0, st));
@@ -176,8 +189,10 @@ int main(int argc, char** argv) {
         const bool ok = pkts == (uint64_t)n_ev * (reps + 1) && c_got == c_ref &&
                         memcmp(r_got.data(), r_ref.data(), (size_t)n * sizeof(rpkt_rec_t)) == 0;
         same = same && ok;
-        printf("%-5s %u stream(s): %8.1f us per pass, %6.0f Mpps%s%s\n", graph ? "graph" : "eager",
-               F.side.empty() ? 1u : (uint32_t)F.side.size(), ms * 1e3 / reps, frames / (ms * 1e3),
+        const std::string what = how == 2 ? std::string("ring call") :
+            std::to_string(F.side.empty() ? 1u : (uint32_t)F.side.size()) + " stream(s)";
+        printf("%-5s %-11s: %8.1f us per pass, %6.0f Mpps%s%s\n", graph ? "graph" : "eager",
+               what.c_str(), ms * 1e3 / reps, frames / (ms * 1e3),
                graph ? (", " + std::to_string(nodes) + " nodes").c_str() : "",
                ok ? "" : "  MISMATCH");
         if (graph) {

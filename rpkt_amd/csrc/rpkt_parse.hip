@@ -90,26 +90,15 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
 // kept in registers, one 16-B store per lane (1 KiB contiguous per wave), no LDS stage.
 // OPTS: also walk each frame's IPv4 and TCP options (rpkt_gpu_parse_options_batch) from
 // the header window the parse holds, between the parse and the L4 stream.
-template <bool L4, int V, bool C16 = false, bool OPTS = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
-void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
-                  const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
-                  uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
-                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
-                  rpkt_opts_t* __restrict__ opts) {
-    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
-    // the option-type rules of both iterators (OPTS; 4 + 4 x 9744 + 512 B: still four
-    // blocks per CU)
-    __shared__ uint8_t opt_rules[OPTS ? 512 : 4];
-    if constexpr (OPTS) {
-        opt_rules_fill(opt_rules);
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wid = threadIdx.x / kWave;
-    WaveScratch& W = scratch[wid];
-    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
-    if (p0 >= n) return;                                          // wave-uniform exit
+// The tile of frames [p0, p0 + 64) of a batch, by one wave with its scratch W (p0 < n).
+template <bool L4, int V, bool C16, bool OPTS>
+__device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_rules,
+                                           const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                                           const uint32_t* __restrict__ offsets, uint32_t stride,
+                                           uint32_t frame_len, uint32_t n, uint32_t flags,
+                                           rpkt_rec_t* __restrict__ recs,
+                                           uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
+                                           rpkt_opts_t* __restrict__ opts, uint32_t p0, int lane) {
     const uint32_t i = p0 + lane;
     const bool valid = i < n;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
@@ -206,6 +195,63 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     } else {
         flush_records<V != 8>(W, lane, recs, p0, n);
     }
+}
+
+template <bool L4, int V, bool C16 = false, bool OPTS = false>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
+void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
+                  const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                  uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
+                  uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
+                  rpkt_opts_t* __restrict__ opts) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    // the option-type rules of both iterators (OPTS; 4 + 4 x 9744 + 512 B: still four
+    // blocks per CU)
+    __shared__ uint8_t opt_rules[OPTS ? 512 : 4];
+    if constexpr (OPTS) {
+        opt_rules_fill(opt_rules);
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    parse_tile<L4, V, C16, OPTS>(scratch[wid], opt_rules, frames, frames_bytes, offsets, stride,
+                                 frame_len, n, flags, recs, flow_ev, n_buckets, opts, p0, lane);
+}
+
+// A receive ring's slots in one launch (rpkt_gpu_parse_ring): wave t takes tile t of the
+// ring's tiles, numbered slot after slot (tile0[k] = the first tile of slot k), and
+// parses it exactly as parse_kernel parses that tile of the slot's own batch.  The slot
+// descriptors are kernel arguments, read with scalar loads.
+constexpr uint32_t kRingMax = RPKT_RING_MAX_SLOTS;
+struct RingSlot {
+    const uint8_t* frames;
+    const uint32_t* offsets;
+    rpkt_rec_t* recs;
+    uint64_t* flow_ev;
+    uint32_t frames_bytes, stride, frame_len, n;
+};
+struct RingArgs {
+    uint32_t n_slots;
+    uint32_t tile0[kRingMax + 1];
+    RingSlot s[kRingMax];
+};
+
+template <bool L4>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t t = blockIdx.x * kWavesPerBlock + wid;
+    if (t >= A.tile0[A.n_slots]) return;                          // wave-uniform exit
+    uint32_t k = 0;                                               // the slot holding tile t
+    for (uint32_t j = 1; j < A.n_slots; ++j) k = A.tile0[j] <= t ? j : k;
+    const RingSlot& S = A.s[k];
+    parse_tile<L4, 0, false, false>(scratch[wid], nullptr, S.frames, S.frames_bytes, S.offsets,
+                                    S.stride, S.frame_len, S.n, flags, S.recs, S.flow_ev, n_buckets,
+                                    nullptr, (t - A.tile0[k]) * kWave, lane);
 }
 
 // ---- mbuf chains: the same parse over rpkt-dpdk's Pbuf ----
@@ -1038,6 +1084,55 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
+}
+
+int rpkt_gpu_parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
+                        uint32_t n_buckets, void* stream) {
+    if (n_slots && !slots) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    const bool fev = (flags & RPKT_F_FLOW_EV) != 0;
+    if (fev && (n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)) return RPKT_E_INVAL;
+    for (uint32_t k = 0; k < n_slots; ++k) {                      // all checked, then launched
+        const rpkt_ring_slot_t& q = slots[k];
+        const rpkt_batch_t& b = q.batch;
+        if (b.n == 0) continue;
+        if (!b.frames_dev || !q.recs_dev) return RPKT_E_INVAL;
+        if (b.frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+        if (!b.offsets_dev && b.stride == 0) return RPKT_E_INVAL;
+        if (((uintptr_t)q.recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+        if (fev && !q.flow_ev_dev) return RPKT_E_INVAL;
+        if (fev && ((uintptr_t)q.flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_ring_kernel<true> : parse_ring_kernel<false>;
+    RingArgs A;
+    uint32_t k0 = 0;
+    while (k0 < n_slots) {
+        A.n_slots = 0;
+        A.tile0[0] = 0;
+        for (; k0 < n_slots && A.n_slots < kRingMax; ++k0) {
+            const rpkt_ring_slot_t& q = slots[k0];
+            const rpkt_batch_t& b = q.batch;
+            if (b.n == 0) continue;
+            RingSlot& S = A.s[A.n_slots];
+            S.frames = b.frames_dev;
+            S.offsets = b.offsets_dev;
+            S.recs = q.recs_dev;
+            S.flow_ev = fev ? (uint64_t*)q.flow_ev_dev : nullptr;
+            S.frames_bytes = (uint32_t)b.frames_bytes;
+            S.stride = b.stride;
+            S.frame_len = b.offsets_dev ? 0u : (b.frame_len ? b.frame_len : b.stride);
+            S.n = b.n;
+            A.tile0[A.n_slots + 1] = A.tile0[A.n_slots] + (b.n + kWave - 1) / kWave;
+            ++A.n_slots;
+        }
+        if (A.n_slots == 0) break;
+        const uint32_t waves = A.tile0[A.n_slots];
+        const int rc = launch(k, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock),
+                              dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, A, flags,
+                              n_buckets);
+        if (rc) return rc;
+    }
+    return RPKT_OK;
 }
 
 int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,

@@ -37,6 +37,11 @@ class Chains(ctypes.Structure):
                 ("n_segs", ctypes.c_uint32), ("n_chains", ctypes.c_uint32)]
 
 
+class RingSlot(ctypes.Structure):
+    """rpkt_ring_slot_t"""
+    _fields_ = [("batch", Batch), ("recs_dev", ctypes.c_void_p), ("flow_ev_dev", ctypes.c_void_p)]
+
+
 class Fwd(ctypes.Structure):
     """rpkt_fwd_t"""
     _fields_ = [("dmac", ctypes.c_uint8 * 6), ("smac", ctypes.c_uint8 * 6),
@@ -52,7 +57,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_options_batch", "rpkt_gpu_layers_batch", "rpkt_gpu_fields_batch",
            "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
            "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact",
-           "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact"]
+           "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
+           "rpkt_gpu_parse_ring"]
 
 _lib = None
 
@@ -82,6 +88,9 @@ def lib():
         L.rpkt_gpu_parse_batch.restype = ctypes.c_int
         L.rpkt_gpu_parse_batch_compact.argtypes = L.rpkt_gpu_parse_batch.argtypes
         L.rpkt_gpu_parse_batch_compact.restype = ctypes.c_int
+        L.rpkt_gpu_parse_ring.argtypes = [ctypes.POINTER(RingSlot), ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.rpkt_gpu_parse_ring.restype = ctypes.c_int
         L.rpkt_gpu_flow_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.rpkt_gpu_flow_workspace_bytes.restype = ctypes.c_size_t
         L.rpkt_gpu_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
@@ -246,6 +255,25 @@ def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, st
                                             n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_batch_compact")
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
+
+
+def ring_slots(batches, recs, flow_evs=None):
+    """The rpkt_ring_slot_t array of a receive ring: batch k, its record tensor and
+    (optional) its flow-event tensor.  Build it once per ring and pass it to parse_ring
+    on every pass: it holds device addresses only."""
+    arr = (RingSlot * len(batches))()
+    for k, (db, r) in enumerate(zip(batches, recs)):
+        arr[k].batch = db.desc()
+        arr[k].recs_dev = r.data_ptr()
+        arr[k].flow_ev_dev = flow_evs[k].data_ptr() if flow_evs is not None else None
+    return arr
+
+
+def parse_ring(slots, flags=3, n_buckets=0, stream=None):
+    """rpkt_gpu_parse_ring: every slot of `slots` (ring_slots()) parsed as by parse_batch,
+    RPKT_RING_MAX_SLOTS slots per kernel launch."""
+    rc = lib().rpkt_gpu_parse_ring(slots, len(slots), flags, n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_ring")
 
 
 def flow_workspace(n, n_buckets, device="cuda"):

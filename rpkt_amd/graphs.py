@@ -7,6 +7,9 @@ small batches is launch-bound: the engine's calls are kernel launches and nothin
 (no allocation, no synchronisation, no host round trip), so a pass of the loop can be
 captured as one hipGraph and replayed with one host call.
 
+A pass that parses its slots with one rpkt_gpu_parse_ring call (`rx_pass_ring`) needs
+no graph to avoid the per-batch launches: the ring's slots are one kernel.
+
 `CapturedLoop(fn)` runs `fn` once eagerly (the warm pass, which also does the engine's
 one-time per-device setup outside the capture), captures a second call of `fn` into a
 graph (torch.cuda.CUDAGraph, a hipGraph on ROCm) and `replay()`s it.  `fn` issues its
@@ -61,3 +64,11 @@ def rx_pass(ring, recs, ev_all, counters, ws, flags, n_buckets, streams=None):
     for s in streams or ():
         cur.wait_stream(s)
     engine.flow_count(ev_all[:off], off, n_buckets, counters=counters, workspace=ws)
+
+
+def rx_pass_ring(slots, ev_all, n_ev, counters, ws, flags, n_buckets):
+    """The same pass with the slots parsed by one rpkt_gpu_parse_ring call
+    (engine.ring_slots(ring, recs, event views) built once per ring): one kernel for up
+    to RPKT_RING_MAX_SLOTS slots instead of one per slot."""
+    engine.parse_ring(slots, flags | engine.F_FLOW_EV, n_buckets)
+    engine.flow_count(ev_all[:n_ev], n_ev, n_buckets, counters=counters, workspace=ws)

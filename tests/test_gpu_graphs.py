@@ -79,6 +79,33 @@ def test_captured_rx_loop_matches_eager_and_oracle(torch, n_streams):
     assert int(got.reshape(-1, 4)[:, 0].sum()) == passes * n_ev
 
 
+def test_captured_ring_call(torch):
+    """The pass with its slots parsed by one rpkt_gpu_parse_ring call, captured and
+    replayed, counts what the per-slot pass counts."""
+    nb, passes = 1024, 3
+    hbs = [gen.make_batch(2 if k % 2 == 0 else 4, 2000 + 301 * k, seed=700 + k) for k in range(5)]
+    ring = [engine.DeviceBatch.from_host(h) for h in hbs]
+    n_ev = sum(h.n for h in hbs)
+    recs, ev_all = _ring_buffers(torch, ring)
+    offs = np.cumsum([0] + [h.n for h in hbs])
+    slots = engine.ring_slots(ring, recs, [ev_all[offs[k]:offs[k + 1]] for k in range(len(hbs))])
+    cnt = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
+    ws = engine.flow_workspace(n_ev, nb)
+    loop = graphs.CapturedLoop(lambda: graphs.rx_pass_ring(slots, ev_all, n_ev, cnt, ws, 3, nb))
+    for _ in range(passes - 1):
+        loop.replay()
+    recs_e, ev_e = _ring_buffers(torch, ring)
+    cnt_e = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
+    ws_e = engine.flow_workspace(n_ev, nb)
+    for _ in range(passes):
+        graphs.rx_pass(ring, recs_e, ev_e, cnt_e, ws_e, 3, nb)
+    torch.cuda.synchronize()
+    assert torch.equal(cnt, cnt_e)
+    assert torch.equal(ev_all, ev_e)
+    for a, b in zip(recs, recs_e):
+        assert torch.equal(a, b)
+
+
 def test_replay_reads_refilled_slots(torch):
     """The graph bakes in buffer addresses, not contents: a slot refilled between replays
     (as a NIC refills its ring) is parsed from its new frames."""
@@ -136,4 +163,4 @@ def test_cpp_host_captures_the_abi(torch):
     out = subprocess.run([exe, "8192", "8", "5", "3"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "counters and records identical in every mode: yes" in out.stdout
-    assert out.stdout.count("Mpps") == 4
+    assert out.stdout.count("Mpps") == 6

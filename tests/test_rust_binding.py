@@ -65,6 +65,17 @@ def rust_structs():
     return out
 
 
+def rust_align(t):
+    a = re.fullmatch(r"\[(\w+);.*\]", t)
+    if a:
+        return RUST_SCALARS[a.group(1)]
+    if t.startswith("*"):
+        return 8
+    if t in RUST_SCALARS:
+        return RUST_SCALARS[t]
+    return max(rust_align(ft) for _, ft in rust_structs()[t])      # a nested struct
+
+
 def rust_size(t):
     a = re.fullmatch(r"\[(\w+);\s*(\w+)\]", t)
     if a:
@@ -72,7 +83,12 @@ def rust_size(t):
         return RUST_SCALARS[a.group(1)] * n
     if t.startswith("*"):
         return 8
-    return RUST_SCALARS[t]
+    if t in RUST_SCALARS:
+        return RUST_SCALARS[t]
+    fields = rust_structs()[t]                                        # a nested struct
+    _, off, size = rust_layout(fields)[-1]
+    al = rust_align(t)
+    return (off + size + al - 1) // al * al
 
 
 def rust_layout(fields):
@@ -80,8 +96,7 @@ def rust_layout(fields):
     off, out = 0, []
     for f, t in fields:
         size = rust_size(t)
-        a = re.fullmatch(r"\[(\w+);.*\]", t)
-        align = RUST_SCALARS[a.group(1)] if a else min(size, 8)
+        align = rust_align(t)
         off = (off + align - 1) // align * align
         out.append((f, off, size))
         off += size
@@ -139,8 +154,7 @@ def test_struct_layouts_match_c(c_layout):
                 s, f, off, size, c_layout[(s, f)])
         last_f, last_off, last_size = lay[-1]
         end = last_off + last_size
-        align = max(min(rust_size(t), 8) if not t.startswith("[") else
-                    RUST_SCALARS[re.fullmatch(r"\[(\w+);.*\]", t).group(1)] for _, t in fields)
+        align = max(rust_align(t) for _, t in fields)
         assert (end + align - 1) // align * align == c_layout[(s, "__size__")], s
 
 
