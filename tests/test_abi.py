@@ -166,6 +166,32 @@ def test_argument_validation_without_launch(L):
     assert L.rpkt_gpu_flow_workspace_bytes(1 << 20, 8192) > 0
 
 
+def test_ring_argument_validation_without_launch(L):
+    """rpkt_gpu_parse_ring checks every slot before it launches anything; a ring of
+    empty slots launches nothing."""
+    S = (engine.RingSlot * 3)()
+    P = ctypes.cast(S, ctypes.POINTER(engine.RingSlot))
+    assert L.rpkt_gpu_parse_ring(None, 1, 3, 0, None) == -1                   # NULL slots
+    assert L.rpkt_gpu_parse_ring(None, 0, 3, 0, None) == 0                    # nothing to do
+    assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == 0                       # all n == 0
+    assert L.rpkt_gpu_parse_ring(P, 3, 0x80, 0, None) == -1                   # bad flag
+    assert L.rpkt_gpu_parse_ring(P, 3, 7, 0, None) == -1                      # FLOW_EV, 0 buckets
+    S[1].batch = engine.Batch(4096, 640, None, 64, 0, 10, 0)
+    S[1].recs_dev = 16
+    S[2].batch = engine.Batch(4096, 1 << 32, None, 64, 0, 10, 0)
+    S[2].recs_dev = 16
+    assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == -3                      # slot 2 > 4 GiB
+    S[2].batch.frames_bytes = 640
+    S[2].recs_dev = 24
+    assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == -4                      # slot 2 misaligned
+    S[2].recs_dev = 32
+    assert L.rpkt_gpu_parse_ring(P, 3, 7, 64, None) == -1                     # no flow events
+    S[1].flow_ev_dev, S[2].flow_ev_dev = 64, 68
+    assert L.rpkt_gpu_parse_ring(P, 3, 7, 64, None) == -4                     # events misaligned
+    S[2].batch.stride = 0
+    assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == -1                      # no layout
+
+
 def test_engine_refuses_cpu_fallback():
     import torch
     if torch.cuda.is_available():
