@@ -328,16 +328,16 @@ def oracle_for_baseline():
 
 
 def timed_reps(fn, seconds):
-    """Run fn() once to size the loop, then repeat it for >= `seconds`; returns
-    (reps, elapsed)."""
-    t0 = time.perf_counter()
+    """Run fn() once (cold: caches, page faults), then repeat it until >= `seconds` have
+    passed; returns (reps, elapsed)."""
     fn()
-    one = time.perf_counter() - t0
-    reps = max(1, int(seconds / max(one, 1e-6)))
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    reps, t0 = 0, time.perf_counter()
+    while True:
         fn()
-    return reps, time.perf_counter() - t0
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return reps, dt
 
 
 def cpu_fields(value_mpps, gbs, threads, sample, reps, dt, build):
