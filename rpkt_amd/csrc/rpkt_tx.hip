@@ -7,6 +7,9 @@ namespace {
 #ifndef RPKT_BUILD_WIN_AUX
 #define RPKT_BUILD_WIN_AUX 0     // cache policy of build_kernel's window loads (2 = nt)
 #endif
+#ifndef RPKT_BUILD_REC_NT
+#define RPKT_BUILD_REC_NT 1      // build_kernel's record loads non-temporal (read once)
+#endif
 #ifndef RPKT_TX_W64_ON
 #define RPKT_TX_W64_ON 1         // hand short strided batches to the 64-B-window compile
 #endif
@@ -199,7 +202,8 @@ __device__ __forceinline__ void load_records_tile(const rpkt_rec_t* recs, uint32
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         const uint32_t c = k * kWave + lane;
-        v[k] = (c / 5 < nrec) ? in[c] : u32x4{0u, 0u, 0u, 0u};
+        v[k] = (c / 5 < nrec) ? (RPKT_BUILD_REC_NT ? __builtin_nontemporal_load(&in[c]) : in[c])
+                              : u32x4{0u, 0u, 0u, 0u};
     }
     uint32_t* st = rec_stage(W);
 #pragma unroll
