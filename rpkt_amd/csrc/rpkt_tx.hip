@@ -336,6 +336,9 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
 // V: ablation variant for tools/ablate.py (0 = the product kernel; 1 = no write-back,
 // 2 = parse without the L4 sum, 3 = window + write-back of the whole frame only,
 // 4 = default-policy window loads).
+#ifndef RPKT_FWD_WB_AUX
+#define RPKT_FWD_WB_AUX 3        // forward's write-back stores: sc0 | nt
+#endif
 #ifndef RPKT_FWD_WAVES_W64
 #define RPKT_FWD_WAVES_W64 5     // 64-B windows: LDS allows 6 waves per SIMD; 5 -> <= 96 VGPRs
 #endif
@@ -456,7 +459,7 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     // the rewritten lines are not read again: streaming stores (forward 2: 27.8 -> 26.2 us
     // same process; build keeps the default policy, build 3 +2.5 % with it,
     // profiles/r02_ab_wb)
-    if constexpr (V != 1) write_back<3>(rs, frames, W, lane, fr.off, r1);
+    if constexpr (V != 1) write_back<RPKT_FWD_WB_AUX>(rs, frames, W, lane, fr.off, r1);
     if (valid) keep[i] = fwd_ok ? 1 : 0;
 }
 
