@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 COUNTERS=${COUNTERS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS}
 timeout -s KILL 120 rocprofv3 --pmc $COUNTERS \
     -T --output-format csv -d "$OUT" -o sq \
-    -- python3 "$R/bench.py" --no-cpu --config "$CFG" --also "" --tx "" --compact "" --strong "" --opts "" --host "" --steps 10 --warmup 2 --min-warmup-s 0 "${@:4}" > "$OUT/bench.log" 2>&1
+    -- python3 "$R/bench.py" --no-cpu --config "$CFG" --also "" --tx "" --compact "" --strong "" --opts "" --host "" --rx-graph "" --steps 10 --warmup 2 --min-warmup-s 0 "${@:4}" > "$OUT/bench.log" 2>&1
 python3 - "$OUT" "$KERNEL" <<'PY'
 import csv, collections, sys, json
 rows = list(csv.DictReader(open(sys.argv[1] + "/sq_counter_collection.csv")))
