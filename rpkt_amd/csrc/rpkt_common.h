@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <tuple>
+#include <type_traits>
 
 #include "../../include/rpkt_gpu.h"
 
@@ -145,6 +146,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
+// Inclusive max-scan over the 64 lanes (the same DPP pattern; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
     return __builtin_amdgcn_readlane(wave_incl_scan(x), 63);
 }
@@ -216,7 +228,23 @@ struct StreamBatch {
 // current chunk, its chunk span [p0, p1), and off = ceil16(s_q) - 16 * p0, so chunk c
 // of range q is at off + 16 c.  The ranges are in chunk order, so a cursor only moves
 // forward: one step to the next range, binary search only for jumps.
-struct StreamCursor { uint32_t q, p0, p1, off; };
+// Short ranges (under 64 chunks on average: packed IMIX-like tiles) make most steps
+// jump, and a wave then runs the six dependent LDS reads of the search on nearly every
+// chunk (config 4: a lane jumps on 71 % of its steps, some lane of the wave on 89 %).
+// There the owners come from marks instead (MARKS): each range whose first chunk falls
+// in the wave's current 64-chunk window writes its index + 1 at that position of a
+// 64-entry LDS row (W.e, free during the stream), every lane reads its position, and an
+// inclusive max-scan across the lanes carries each range to the chunks after its start,
+// with the last owner of the window before as the floor.  No search, no branch.
+struct StreamCursor {
+    uint32_t q, p0, p1, off;
+    uint32_t my_p0;            // MARKS: this lane's range: first chunk, and
+    bool my_has;               //   whether it has any
+    uint32_t carry;            // MARKS: owner + 1 of the previous window's last chunk
+};
+#ifndef RPKT_STREAM_MARKS
+#define RPKT_STREAM_MARKS 1      // 0: the cursor with binary search on every tile
+#endif
 
 __device__ __forceinline__ void cursor_load(const WaveScratch& W, StreamCursor& k, uint32_t q) {
     k.q = q;
@@ -225,14 +253,29 @@ __device__ __forceinline__ void cursor_load(const WaveScratch& W, StreamCursor& 
     k.off = W.s[q];
 }
 
-template <int AUX, int U>
+template <int AUX, int U, bool MARKS>
 __device__ __forceinline__ void stream_issue(__amdgpu_buffer_rsrc_t rs, uint32_t oob,
-                                             const WaveScratch& W, uint32_t total, uint32_t base,
+                                             WaveScratch& W, uint32_t total, uint32_t base,
                                              int lane, StreamCursor& k, StreamBatch<U>& B) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint32_t c = base + u * kWave + lane;
         const bool valid = c < total;
+        if constexpr (MARKS) {
+            const uint32_t rel = k.my_p0 - (base + u * kWave);     // the window's start: uniform
+            if (k.my_has && rel < (uint32_t)kWave) W.e[rel] = (uint32_t)lane + 1u;
+            __builtin_amdgcn_wave_barrier();                       // LDS is in order per wave
+            const uint32_t mk = W.e[lane];
+            W.e[lane] = 0u;                                        // clear for the next window
+            uint32_t v = wave_incl_max(mk);
+            v = v > k.carry ? v : k.carry;
+            k.carry = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+            const uint32_t q = valid ? v - 1u : 0u;
+            const uint32_t p0 = W.pref[q], p1 = W.pref[q + 1];
+            B.m[u] = q | ((uint32_t)(c == p0) << 8) | ((uint32_t)(c + 1 == p1) << 9);
+            B.d[u] = load16_fast<AUX>(rs, valid ? W.s[q] + 16u * c : oob);
+            continue;
+        }
         if (valid && k.p1 <= c) {
             uint32_t q = k.q + 1;
             if (W.pref[q + 1] <= c) {
@@ -308,6 +351,7 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
     W.pref[lane] = incl - nch;
     if (lane == 63) W.pref[64] = incl;
     W.s[lane] = S - 16u * (incl - nch);
+    W.e[lane] = 0;
     W.first[lane] = 0;
     W.last[lane] = 0;
     wave_sync();
@@ -316,18 +360,29 @@ __device__ __forceinline__ uint32_t wave_stream_sum(__amdgpu_buffer_rsrc_t rs, u
     uint32_t run = 0;
     StreamCursor k;
     cursor_load(W, k, 0);
+    k.my_p0 = incl - nch;
+    k.my_has = nch != 0;
+    k.carry = 0;
     StreamBatch<U> A, B;
     uint32_t base = 0;
-    stream_issue<AUX, U>(rs, oob, W, total, base, lane, k, A);
-    const uint32_t edge = edges();
-    for (;;) {
-        stream_issue<AUX, U>(rs, oob, W, total, base + kBatch, lane, k, B);
-        stream_consume<U>(W, run, A);
-        stream_issue<AUX, U>(rs, oob, W, total, base + 2 * kBatch, lane, k, A);
-        stream_consume<U>(W, run, B);
-        base += 2 * kBatch;
-        if (base >= total) break;
-    }
+    // the loop, with the owners from marks (short ranges) or from the cursor
+    auto loop = [&](auto marks) -> uint32_t {
+        constexpr bool M = decltype(marks)::value;
+        stream_issue<AUX, U, M>(rs, oob, W, total, base, lane, k, A);
+        const uint32_t edge = edges();
+        for (;;) {
+            stream_issue<AUX, U, M>(rs, oob, W, total, base + kBatch, lane, k, B);
+            stream_consume<U>(W, run, A);
+            stream_issue<AUX, U, M>(rs, oob, W, total, base + 2 * kBatch, lane, k, A);
+            stream_consume<U>(W, run, B);
+            base += 2 * kBatch;
+            if (base >= total) break;
+        }
+        return edge;
+    };
+    const uint32_t edge = (RPKT_STREAM_MARKS && total < 64u * kWave)            // uniform
+                              ? loop(std::integral_constant<bool, true>{})
+                              : loop(std::integral_constant<bool, false>{});
     wave_sync();
     return (nch ? W.last[lane] - W.first[lane] : 0) + edge;
 }
