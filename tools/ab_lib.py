@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3]
+Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7]
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -58,13 +58,19 @@ def main():
     B = ctypes.CDLL(os.path.abspath(args.lib_b))
     mode, cfg = args.leg.rstrip("0123456789"), int(args.leg[len(args.leg.rstrip("0123456789")):])
     R = args.rotate or (8 if cfg == 2 else 1)    # 8 x 64 MiB of frames: past the 256 MiB cache
-    hbs = [gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else
-           gen.make_batch(cfg, args.n or None, seed=gen.DEFAULT_SEED[cfg] + 104729 * r)
-           for r in range(R)]
+    if mode == "chains":                         # mbuf chains (configs 7, 8)
+        hbs = [gen.make_chains(cfg, args.n or None)]
+        dbs = [engine.DeviceChains.from_host(h) for h in hbs]
+        recss = []
+    else:
+        hbs = [gen.make_mix(seed=gen.DEFAULT_SEED[9]) if cfg == 9 else
+               gen.make_batch(cfg, args.n or None, seed=gen.DEFAULT_SEED[cfg] + 104729 * r)
+               for r in range(R)]
+        dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
+        recss = [engine.parse_batch(d, 3) for d in dbs]
+    R = len(hbs)
     hb = hbs[0]
-    dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
     descs = [d.desc() for d in dbs]
-    recss = [engine.parse_batch(d, 3) for d in dbs]
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
     P = ctypes.POINTER(engine.Batch)
@@ -113,6 +119,13 @@ def main():
             flags = 1 if cfg == 2 else 3
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
+        elif mode == "chains":                      # rpkt_gpu_parse_chains, both sums
+            L.rpkt_gpu_parse_chains.argtypes = [ctypes.POINTER(engine.Chains), ctypes.c_uint32,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_void_p]
+            out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
+            call[name] = (lambda k, L=L, out=out: L.rpkt_gpu_parse_chains(
+                ctypes.byref(descs[0]), 3, out.data_ptr(), None, 0, sp))
         elif mode == "parsec":                      # compact records
             L.rpkt_gpu_parse_batch_compact.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p,
                                                        ctypes.c_void_p, ctypes.c_uint32,
