@@ -566,10 +566,7 @@ template <bool L4>
 // A long chain makes a wave's item stream long and the grid small (256K 8000-B
 // chains = 4096 waves, one per SIMD): the stream keeps kChainStreamUnroll loads per
 // lane per batch in flight, and registers, not waves, are the budget (<= 256).
-#ifndef RPKT_CHAINS_BLOCKS
-#define RPKT_CHAINS_BLOCKS 2     // blocks per CU the chains kernel is compiled for (VGPR budget)
-#endif
-__global__ __launch_bounds__(kWave * kWavesPerBlock, RPKT_CHAINS_BLOCKS)
+__global__ __launch_bounds__(kWave * kWavesPerBlock, 2)
 void parse_chains_kernel(const uint8_t* __restrict__ buf, uint32_t fb,
                          const uint2* __restrict__ segs, uint32_t n_segs,
                          const uint32_t* __restrict__ chain_first, uint32_t n, uint32_t flags,
