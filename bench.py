@@ -599,13 +599,20 @@ def run_rx_graph(args):
         ev_all = torch.empty(n * slots, dtype=torch.int64, device="cuda")
         ws = engine.flow_workspace(n * slots, nb)
         side = [torch.cuda.Stream() for _ in range(4)]
-        rslots = engine.ring_slots(ring, recs, [ev_all[k * n:(k + 1) * n] for k in range(slots)])
+        evs = [ev_all[k * n:(k + 1) * n] for k in range(slots)]
+        rslots = engine.ring_slots(ring, recs, evs)
+        recs16 = [torch.empty(n * REC16_BYTES, dtype=torch.uint8, device="cuda") for _ in range(slots)]
+        rslots16 = engine.ring_slots(ring, recs16, evs)
         res, cnts = {}, []
-        for mode in ("eager", "graph", "eager_4streams", "graph_4streams", "ring", "ring_graph"):
+        for mode in ("eager", "graph", "eager_4streams", "graph_4streams", "ring", "ring_graph",
+                     "ring_compact"):
             cnt = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
             cnts.append(cnt)
             streams = side if mode.endswith("4streams") else None
-            if mode.startswith("ring"):
+            if mode == "ring_compact":
+                fn = (lambda cnt=cnt: graphs.rx_pass_ring(rslots16, ev_all, n * slots, cnt, ws,
+                                                          gen.FLAGS[2], nb, compact=True))
+            elif mode.startswith("ring"):
                 fn = (lambda cnt=cnt: graphs.rx_pass_ring(rslots, ev_all, n * slots, cnt, ws,
                                                           gen.FLAGS[2], nb))
             else:
@@ -630,7 +637,7 @@ def run_rx_graph(args):
         out["%dx%d" % (n, slots)] = {
             k: ({kk: round(vv, 3) for kk, vv in v.items()} if isinstance(v, dict) else v)
             for k, v in res.items()}
-        del ring, recs, ev_all
+        del ring, recs, recs16, ev_all
         torch.cuda.empty_cache()
     return out
 

@@ -136,7 +136,8 @@ pub struct rpkt_batch_t {
 #[derive(Clone, Copy, Debug)]
 pub struct rpkt_ring_slot_t {
     pub batch: rpkt_batch_t,
-    pub recs_dev: *mut rpkt_rec_t,
+    /// `*mut rpkt_rec_t` for rpkt_gpu_parse_ring, `*mut rpkt_rec16_t` for the compact call
+    pub recs_dev: *mut c_void,
     pub flow_ev_dev: *mut rpkt_flow_ev_t,
 }
 pub const RPKT_RING_MAX_SLOTS: u32 = 32;
@@ -240,9 +241,12 @@ extern "C" {
                                         flow_ev_dev: *mut rpkt_flow_ev_t, n_buckets: u32,
                                         stream: *mut c_void) -> c_int;
 
-    /// Every slot parsed as by rpkt_gpu_parse_batch, RPKT_RING_MAX_SLOTS slots per launch.
+    /// Every slot parsed as by rpkt_gpu_parse_batch (or _compact), RPKT_RING_MAX_SLOTS
+    /// slots per launch.
     pub fn rpkt_gpu_parse_ring(slots: *const rpkt_ring_slot_t, n_slots: u32, flags: u32,
                                n_buckets: u32, stream: *mut c_void) -> c_int;
+    pub fn rpkt_gpu_parse_ring_compact(slots: *const rpkt_ring_slot_t, n_slots: u32, flags: u32,
+                                       n_buckets: u32, stream: *mut c_void) -> c_int;
 
     pub fn rpkt_gpu_flow_workspace_bytes(n: u32, n_buckets: u32) -> usize;
     pub fn rpkt_gpu_flow_count(flow_ev_dev: *const rpkt_flow_ev_t, n: u32, n_buckets: u32,

@@ -219,15 +219,19 @@ int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* batch, uint32_t flags,
  * rpkt_gpu_parse_batch call per slot (records into each slot's recs_dev, flow events into
  * its flow_ev_dev when RPKT_F_FLOW_EV is set), but small batches no longer pay a
  * dependent kernel launch each.  Slots with n == 0 are skipped; every slot is checked
- * before anything is launched.  Layouts may differ from slot to slot. */
+ * before anything is launched.  Layouts may differ from slot to slot.  recs_dev points to
+ * rpkt_rec_t records for rpkt_gpu_parse_ring and to rpkt_rec16_t records for
+ * rpkt_gpu_parse_ring_compact (equal to rpkt_gpu_parse_batch_compact per slot). */
 typedef struct rpkt_ring_slot {
     rpkt_batch_t    batch;
-    rpkt_rec_t*     recs_dev;
+    void*           recs_dev;
     rpkt_flow_ev_t* flow_ev_dev;
 } rpkt_ring_slot_t;
 #define RPKT_RING_MAX_SLOTS 32u
 int rpkt_gpu_parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
                         uint32_t n_buckets, void* stream);
+int rpkt_gpu_parse_ring_compact(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
+                                uint32_t n_buckets, void* stream);
 
 /* Accumulate flow events into counters_dev (u64[(n_buckets+1)*4], caller
  * zeroes it once; calls add).  workspace_dev must hold

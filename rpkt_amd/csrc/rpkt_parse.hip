@@ -238,7 +238,7 @@ struct RingArgs {
     RingSlot s[kRingMax];
 };
 
-template <bool L4>
+template <bool L4, bool C16>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
 void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
@@ -249,7 +249,7 @@ void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
     uint32_t k = 0;                                               // the slot holding tile t
     for (uint32_t j = 1; j < A.n_slots; ++j) k = A.tile0[j] <= t ? j : k;
     const RingSlot& S = A.s[k];
-    parse_tile<L4, 0, false, false>(scratch[wid], nullptr, S.frames, S.frames_bytes, S.offsets,
+    parse_tile<L4, 0, C16, false>(scratch[wid], nullptr, S.frames, S.frames_bytes, S.offsets,
                                     S.stride, S.frame_len, S.n, flags, S.recs, S.flow_ev, n_buckets,
                                     nullptr, (t - A.tile0[k]) * kWave, lane);
 }
@@ -1010,6 +1010,56 @@ int parse_options(const rpkt_batch_t* b, uint32_t flags, void* recs_dev, rpkt_op
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets, opts_dev);
 }
 
+template <bool C16>
+int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
+                      uint32_t n_buckets, void* stream) {
+    if (n_slots && !slots) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    const bool fev = (flags & RPKT_F_FLOW_EV) != 0;
+    if (fev && (n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)) return RPKT_E_INVAL;
+    for (uint32_t k = 0; k < n_slots; ++k) {                      // all checked, then launched
+        const rpkt_ring_slot_t& q = slots[k];
+        const rpkt_batch_t& b = q.batch;
+        if (b.n == 0) continue;
+        if (!b.frames_dev || !q.recs_dev) return RPKT_E_INVAL;
+        if (b.frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+        if (!b.offsets_dev && b.stride == 0) return RPKT_E_INVAL;
+        if (((uintptr_t)q.recs_dev & 15u) != 0) return RPKT_E_ALIGN;
+        if (fev && !q.flow_ev_dev) return RPKT_E_INVAL;
+        if (fev && ((uintptr_t)q.flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_ring_kernel<true, C16> : parse_ring_kernel<false, C16>;
+    RingArgs A;
+    uint32_t k0 = 0;
+    while (k0 < n_slots) {
+        A.n_slots = 0;
+        A.tile0[0] = 0;
+        for (; k0 < n_slots && A.n_slots < kRingMax; ++k0) {
+            const rpkt_ring_slot_t& q = slots[k0];
+            const rpkt_batch_t& b = q.batch;
+            if (b.n == 0) continue;
+            RingSlot& S = A.s[A.n_slots];
+            S.frames = b.frames_dev;
+            S.offsets = b.offsets_dev;
+            S.recs = (rpkt_rec_t*)q.recs_dev;
+            S.flow_ev = fev ? (uint64_t*)q.flow_ev_dev : nullptr;
+            S.frames_bytes = (uint32_t)b.frames_bytes;
+            S.stride = b.stride;
+            S.frame_len = b.offsets_dev ? 0u : (b.frame_len ? b.frame_len : b.stride);
+            S.n = b.n;
+            A.tile0[A.n_slots + 1] = A.tile0[A.n_slots] + (b.n + kWave - 1) / kWave;
+            ++A.n_slots;
+        }
+        if (A.n_slots == 0) break;
+        const uint32_t waves = A.tile0[A.n_slots];
+        const int rc = launch(k, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock),
+                              dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, A, flags,
+                              n_buckets);
+        if (rc) return rc;
+    }
+    return RPKT_OK;
+}
+
 }  // namespace
 
 // This unit compiles twice: as is (128-B windows) and with RPKT_PARSE_W64 (RPKT_WIN 64,
@@ -1088,51 +1138,12 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
 
 int rpkt_gpu_parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
                         uint32_t n_buckets, void* stream) {
-    if (n_slots && !slots) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
-    const bool fev = (flags & RPKT_F_FLOW_EV) != 0;
-    if (fev && (n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)) return RPKT_E_INVAL;
-    for (uint32_t k = 0; k < n_slots; ++k) {                      // all checked, then launched
-        const rpkt_ring_slot_t& q = slots[k];
-        const rpkt_batch_t& b = q.batch;
-        if (b.n == 0) continue;
-        if (!b.frames_dev || !q.recs_dev) return RPKT_E_INVAL;
-        if (b.frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
-        if (!b.offsets_dev && b.stride == 0) return RPKT_E_INVAL;
-        if (((uintptr_t)q.recs_dev & 15u) != 0) return RPKT_E_ALIGN;
-        if (fev && !q.flow_ev_dev) return RPKT_E_INVAL;
-        if (fev && ((uintptr_t)q.flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
-    }
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_ring_kernel<true> : parse_ring_kernel<false>;
-    RingArgs A;
-    uint32_t k0 = 0;
-    while (k0 < n_slots) {
-        A.n_slots = 0;
-        A.tile0[0] = 0;
-        for (; k0 < n_slots && A.n_slots < kRingMax; ++k0) {
-            const rpkt_ring_slot_t& q = slots[k0];
-            const rpkt_batch_t& b = q.batch;
-            if (b.n == 0) continue;
-            RingSlot& S = A.s[A.n_slots];
-            S.frames = b.frames_dev;
-            S.offsets = b.offsets_dev;
-            S.recs = q.recs_dev;
-            S.flow_ev = fev ? (uint64_t*)q.flow_ev_dev : nullptr;
-            S.frames_bytes = (uint32_t)b.frames_bytes;
-            S.stride = b.stride;
-            S.frame_len = b.offsets_dev ? 0u : (b.frame_len ? b.frame_len : b.stride);
-            S.n = b.n;
-            A.tile0[A.n_slots + 1] = A.tile0[A.n_slots] + (b.n + kWave - 1) / kWave;
-            ++A.n_slots;
-        }
-        if (A.n_slots == 0) break;
-        const uint32_t waves = A.tile0[A.n_slots];
-        const int rc = launch(k, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock),
-                              dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, A, flags,
-                              n_buckets);
-        if (rc) return rc;
-    }
-    return RPKT_OK;
+    return parse_ring<false>(slots, n_slots, flags, n_buckets, stream);
+}
+
+int rpkt_gpu_parse_ring_compact(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
+                                uint32_t n_buckets, void* stream) {
+    return parse_ring<true>(slots, n_slots, flags, n_buckets, stream);
 }
 
 int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,

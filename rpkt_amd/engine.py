@@ -58,7 +58,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
            "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact",
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
-           "rpkt_gpu_parse_ring"]
+           "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact"]
 
 _lib = None
 
@@ -91,6 +91,8 @@ def lib():
         L.rpkt_gpu_parse_ring.argtypes = [ctypes.POINTER(RingSlot), ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
         L.rpkt_gpu_parse_ring.restype = ctypes.c_int
+        L.rpkt_gpu_parse_ring_compact.argtypes = L.rpkt_gpu_parse_ring.argtypes
+        L.rpkt_gpu_parse_ring_compact.restype = ctypes.c_int
         L.rpkt_gpu_flow_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.rpkt_gpu_flow_workspace_bytes.restype = ctypes.c_size_t
         L.rpkt_gpu_flow_count.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
@@ -269,11 +271,13 @@ def ring_slots(batches, recs, flow_evs=None):
     return arr
 
 
-def parse_ring(slots, flags=3, n_buckets=0, stream=None):
-    """rpkt_gpu_parse_ring: every slot of `slots` (ring_slots()) parsed as by parse_batch,
+def parse_ring(slots, flags=3, n_buckets=0, stream=None, compact=False):
+    """rpkt_gpu_parse_ring[_compact]: every slot of `slots` (ring_slots(), with 80-B or,
+    compact, 16-B record tensors) parsed as by parse_batch[_compact],
     RPKT_RING_MAX_SLOTS slots per kernel launch."""
-    rc = lib().rpkt_gpu_parse_ring(slots, len(slots), flags, n_buckets, _stream_ptr(stream))
-    _check(rc, "rpkt_gpu_parse_ring")
+    fn = lib().rpkt_gpu_parse_ring_compact if compact else lib().rpkt_gpu_parse_ring
+    rc = fn(slots, len(slots), flags, n_buckets, _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_ring%s" % ("_compact" if compact else ""))
 
 
 def flow_workspace(n, n_buckets, device="cuda"):

@@ -66,9 +66,9 @@ def rx_pass(ring, recs, ev_all, counters, ws, flags, n_buckets, streams=None):
     engine.flow_count(ev_all[:off], off, n_buckets, counters=counters, workspace=ws)
 
 
-def rx_pass_ring(slots, ev_all, n_ev, counters, ws, flags, n_buckets):
-    """The same pass with the slots parsed by one rpkt_gpu_parse_ring call
+def rx_pass_ring(slots, ev_all, n_ev, counters, ws, flags, n_buckets, compact=False):
+    """The same pass with the slots parsed by one rpkt_gpu_parse_ring[_compact] call
     (engine.ring_slots(ring, recs, event views) built once per ring): one kernel for up
     to RPKT_RING_MAX_SLOTS slots instead of one per slot."""
-    engine.parse_ring(slots, flags | engine.F_FLOW_EV, n_buckets)
+    engine.parse_ring(slots, flags | engine.F_FLOW_EV, n_buckets, compact=compact)
     engine.flow_count(ev_all[:n_ev], n_ev, n_buckets, counters=counters, workspace=ws)

@@ -190,6 +190,7 @@ def test_ring_argument_validation_without_launch(L):
     assert L.rpkt_gpu_parse_ring(P, 3, 7, 64, None) == -4                     # events misaligned
     S[2].batch.stride = 0
     assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == -1                      # no layout
+    assert L.rpkt_gpu_parse_ring_compact(P, 3, 3, 0, None) == -1              # the same checks
 
 
 def test_engine_refuses_cpu_fallback():

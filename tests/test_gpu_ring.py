@@ -87,3 +87,24 @@ def test_bad_slot_fails_before_any_launch(torch):
     assert engine.lib().rpkt_gpu_parse_ring(slots, 0, 3, 0, engine._stream_ptr(None)) == 0
     assert engine.lib().rpkt_gpu_parse_ring(None, 1, 3, 0, engine._stream_ptr(None)) == -1
     assert engine.lib().rpkt_gpu_parse_ring(slots, 2, 0x80, 0, engine._stream_ptr(None)) == -1
+
+
+def test_compact_ring_equals_per_slot_compact_parse(torch):
+    """rpkt_gpu_parse_ring_compact: 16-B records, as rpkt_gpu_parse_batch_compact per
+    slot (strided short frames included, which parse_batch_compact hands to its 64-B-window
+    compile)."""
+    sizes = [64, 1, 3000, 0, 129, 5000] * 6
+    cfgs = [2, 4, 5, 3]
+    hbs = [gen.make_batch(cfgs[k % 4], n, seed=300 + k) for k, n in enumerate(sizes)]
+    nb = 256
+    dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
+    recs = [torch.zeros(max(h.n, 1) * 16, dtype=torch.uint8, device="cuda") for h in hbs]
+    evs = [torch.zeros(max(h.n, 1), dtype=torch.int64, device="cuda") for h in hbs]
+    engine.parse_ring(engine.ring_slots(dbs, recs, evs), 3 | engine.F_FLOW_EV, nb, compact=True)
+    torch.cuda.synchronize()
+    for k, (hb, db) in enumerate(zip(hbs, dbs)):
+        if hb.n == 0:
+            continue
+        r1, e1 = engine.parse_batch_compact(db, 3 | engine.F_FLOW_EV, n_buckets=nb)
+        assert torch.equal(recs[k][:hb.n * 16], r1), "slot %d vs parse_batch_compact" % k
+        assert torch.equal(evs[k][:hb.n], e1), "slot %d events" % k
