@@ -262,7 +262,8 @@ def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, st
 def ring_slots(batches, recs, flow_evs=None):
     """The rpkt_ring_slot_t array of a receive ring: batch k, its record tensor and
     (optional) its flow-event tensor.  Build it once per ring and pass it to parse_ring
-    on every pass: it holds device addresses only."""
+    on every pass: it holds device addresses only, so the batches and tensors must stay
+    alive (and in place) as long as the array is used."""
     arr = (RingSlot * len(batches))()
     for k, (db, r) in enumerate(zip(batches, recs)):
         arr[k].batch = db.desc()
