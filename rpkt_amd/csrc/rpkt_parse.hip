@@ -1063,9 +1063,9 @@ int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
 }  // namespace
 
 // This unit compiles twice: as is (128-B windows) and with RPKT_PARSE_W64 (RPKT_WIN 64,
-// rpkt_amd/build.py), whose only entry point is the hidden
-// rpkt_gpu_parse_batch_compact_w64 the first compile hands strided batches of short
-// frames to: every frame lies inside its 64-B window (parse_w64_fits), so the headers
+// rpkt_amd/build.py), whose only entry points are the hidden
+// rpkt_gpu_parse_batch_compact_w64 / rpkt_gpu_parse_ring_compact_w64 the first compile
+// hands strided batches (rings of them) of short frames to: every frame lies inside its 64-B window (parse_w64_fits), so the headers
 // and the L4 bytes are all in LDS, a wave's LDS drops from 9.7 to 6.5 KB (the window
 // area keeps the 64 x 21-dword record stage's 5376 B), and with the 16-B records kept in
 // registers the VGPRs, not the LDS, set the waves per SIMD.
@@ -1076,6 +1076,11 @@ int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
 extern "C" {
 
 #ifdef RPKT_PARSE_W64
+__attribute__((visibility("hidden"))) int rpkt_gpu_parse_ring_compact_w64(
+    const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags, uint32_t n_buckets,
+    void* stream) {
+    return parse_ring<true>(slots, n_slots, flags, n_buckets, stream);
+}
 __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
     const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
     uint32_t n_buckets, void* stream) {
@@ -1091,6 +1096,7 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
 #else
 int rpkt_gpu_parse_batch_compact_w64(const rpkt_batch_t*, uint32_t, rpkt_rec16_t*,
                                      rpkt_flow_ev_t*, uint32_t, void*);
+int rpkt_gpu_parse_ring_compact_w64(const rpkt_ring_slot_t*, uint32_t, uint32_t, uint32_t, void*);
 
 // every frame of a strided batch inside a 64-B window from its 16-B boundary
 static bool parse_w64_fits(const rpkt_batch_t* b, uint32_t flen) {
@@ -1143,7 +1149,15 @@ int rpkt_gpu_parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_
 
 int rpkt_gpu_parse_ring_compact(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
                                 uint32_t n_buckets, void* stream) {
-    return parse_ring<true>(slots, n_slots, flags, n_buckets, stream);
+    // a ring whose every slot is a strided batch of short frames goes to the 64-B-window
+    // compile, as rpkt_gpu_parse_batch_compact hands such a batch over
+    bool w64 = RPKT_PARSE_W64_ON && slots && n_slots;
+    for (uint32_t k = 0; w64 && k < n_slots; ++k) {
+        const rpkt_batch_t& b = slots[k].batch;
+        w64 = b.n == 0 || parse_w64_fits(&b, b.frame_len ? b.frame_len : b.stride);
+    }
+    return w64 ? rpkt_gpu_parse_ring_compact_w64(slots, n_slots, flags, n_buckets, stream)
+               : parse_ring<true>(slots, n_slots, flags, n_buckets, stream);
 }
 
 int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,

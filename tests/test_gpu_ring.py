@@ -108,3 +108,29 @@ def test_compact_ring_equals_per_slot_compact_parse(torch):
         r1, e1 = engine.parse_batch_compact(db, 3 | engine.F_FLOW_EV, n_buckets=nb)
         assert torch.equal(recs[k][:hb.n * 16], r1), "slot %d vs parse_batch_compact" % k
         assert torch.equal(evs[k][:hb.n], e1), "slot %d events" % k
+
+
+def test_compact_ring_of_short_strided_frames(torch):
+    """A compact ring whose every slot holds strided 64-B frames runs on the 64-B-window
+    compile (as parse_batch_compact does for one such batch); records and events equal
+    the oracle's projected records and events."""
+    from rpkt_amd.records import project16
+    sizes = [1, 64, 65, 0, 4097, 2000, 333]
+    hbs = [gen.make_batch(2, n, seed=900 + k) for k, n in enumerate(sizes)]
+    nb = 128
+    dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
+    recs = [torch.zeros(max(h.n, 1) * 16, dtype=torch.uint8, device="cuda") for h in hbs]
+    evs = [torch.zeros(max(h.n, 1), dtype=torch.int64, device="cuda") for h in hbs]
+    for flags in (1, 3):
+        engine.parse_ring(engine.ring_slots(dbs, recs, evs), flags | engine.F_FLOW_EV, nb,
+                          compact=True)
+        torch.cuda.synchronize()
+        for k, hb in enumerate(hbs):
+            if hb.n == 0:
+                continue
+            o, ev = oracle.parse_batch(hb.frames, hb.n, flags=flags | engine.F_FLOW_EV,
+                                       stride=hb.stride, frame_len=hb.frame_len, n_buckets=nb,
+                                       threads=THREADS, flow_ev=True)
+            want = project16(o, flags).tobytes()
+            assert recs[k][:hb.n * 16].cpu().numpy().tobytes() == want, (flags, k)
+            assert np.array_equal(evs[k][:hb.n].cpu().numpy().view(np.uint64), ev), (flags, k)
