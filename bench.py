@@ -15,6 +15,8 @@ synthetic batch already resident in HBM.
             per-flow counters and one RCCL all-reduce of the counters.
   --config 7: 262,144 x 8000 B jumbo frames as mbuf chains (2048-B segments in
             shuffled 2176-B mempool slots), rpkt_gpu_parse_chains, full L3 + L4 sums.
+  --config 10 / 11: dual stack (RPKT_F_IPV6), 1,048,576 x 64 B IPv4/UDP + IPv6/UDP and
+            1,048,576 x 1500 B IPv4 + IPv6 (0-3 extension headers) TCP/UDP, full sums.
 
   config 1: benches/rpkt's packet_l4 over 1,000 x 64 B frames on the host CPU
             (oracle restatement, 1 thread), ns/pkt under "extra".
@@ -47,12 +49,15 @@ from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, as
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FLAG_NAMES = {1: "ip_sum", 2: "l4_sum", 3: "ip_sum+l4_sum"}
+FLAG_NAMES = {1: "ip_sum", 2: "l4_sum", 3: "ip_sum+l4_sum", 11: "ip_sum+l4_sum+ipv6"}
 WORKLOAD = {2: "1M x 64B Ether/IPv4/UDP extract + IPv4 header checksum",
             3: "1M x 1500B Ether/IPv4/TCP parse + full L3/L4 checksum",
             4: "8M IMIX 64/570/1500 (7:4:1) TCP/UDP, sharded, flow counters + RCCL reduce",
             5: "4M x U[64,1518]B 802.1Q/QinQ + IPv4 options -> TCP options",
-            7: "256K x 8000B jumbo TCP/UDP as 2048-B mbuf chains, parse + full L3/L4 checksum"}
+            7: "256K x 8000B jumbo TCP/UDP as 2048-B mbuf chains, parse + full L3/L4 checksum",
+            10: "1M x 64B dual stack IPv4/UDP + IPv6/UDP parse + full L3/L4 checksum",
+            11: "1M x 1500B dual stack IPv4 + IPv6 (0-3 extension headers) TCP/UDP, full "
+                "L3/L4 checksum"}
 
 
 def log(rank, *a):
@@ -346,6 +351,15 @@ def cpu_fields(value_mpps, gbs, threads, sample, reps, dt, build):
             "sample": sample, "build": build}
 
 
+def flatten_all_cores(out):
+    """SURVEY.md §8(d)(ii), the all-host-cores baseline, as scalars beside the 1-thread
+    value (records that keep only the top level of cpu_baseline still carry it)."""
+    a = out["all_cores"]
+    out.update(all_cores_mpps=a["value"], all_cores_gb_per_s=a["gb_per_s"],
+               all_cores_threads=a["cores"])
+    return out
+
+
 def cpu_baseline_chains(hc, gpu_recs, flags, seconds, threads_all, max_bytes=256 << 20):
     """Chain oracle (oracle/rpkt_oracle_chain.c) over the first chains of the batch
     (~max_bytes of frame data), 1 thread and all usable host threads, each for
@@ -369,7 +383,7 @@ def cpu_baseline_chains(hc, gpu_recs, flags, seconds, threads_all, max_bytes=256
                                     threads_all, "%d reps x %s, %d threads (static partition)"
                                     % (reps_a, sample, threads_all), reps_a, dt_a, build),
                gpu_parity_on_sample=bool(gpu_recs[:m].tobytes() == o.tobytes()))
-    return out
+    return flatten_all_cores(out)
 
 
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
@@ -396,7 +410,7 @@ def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
                                     threads_all, "%d reps x %s, %d threads (static partition)"
                                     % (reps_a, sample, threads_all), reps_a, dt_a, build),
                gpu_parity_on_sample=bool(gpu_recs.tobytes() == o.tobytes()))
-    return out
+    return flatten_all_cores(out)
 
 
 def run_config1(args):
@@ -434,7 +448,8 @@ def layout_name(hb):
     return ("stride%d" % hb.stride) if hb.stride else "packed+u32 offsets"
 
 
-def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, strong=False):
+def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, strong=False,
+               main=False):
     """One parse leg: config `cfg`'s batches resident, K timed launches.  compact: the
     16-byte record entry point (rpkt_gpu_parse_batch_compact) instead of the 80-byte one.
     opts: the fused parse + option walks (rpkt_gpu_parse_options_batch[_compact]), 64 B
@@ -462,7 +477,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         scaling = "weak"
     else:                                          # weak scaling: a batch per rank
         n = args.frames or gen.DEFAULT_N[cfg]
-        R = args.rotate or (8 if cfg == 2 else 1)
+        R = args.rotate or (8 if cfg in (2, 10) else 1)
         hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
                for r in range(R)]
         scaling = "weak"
@@ -545,8 +560,11 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
     # the records of batch 0 are read back before the copy references overwrite them
     g = as_records(recs[0].cpu().numpy()) if cpu and rank == 0 and not compact and not opts \
         else None
-    if cfg == 2 and not compact:
-        out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
+    if cfg == 2 and main and not compact and not strong:
+        try:
+            out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
+        except engine.RpktError as e:           # the development library is optional
+            out["copy_ceiling"] = {"error": str(e)}
     if g is not None:
         if cfg in gen.CHAINED:
             out["cpu_baseline"] = cpu_baseline_chains(hbs[0], g, flags, args.cpu_seconds,
@@ -555,6 +573,58 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
             out["cpu_baseline"] = cpu_baseline(hbs[0], g, flags, args.cpu_seconds,
                                                args.cpu_threads)
     del dbs, recs
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_ring(cfg, args, rank, world, slots=8, compact=False):
+    """A receive ring of `slots` full-size batches of config `cfg` (8 x 1M x 64 B for
+    config 2) parsed by ONE rpkt_gpu_parse_ring[_compact] launch per step: the batch
+    boundary's fixed cost (launch, first-round ramp, last-round drain) is paid once per
+    8M frames instead of once per 1M.  Same batches, flags and records as the headline
+    leg, which parses them one launch per batch."""
+    n = args.frames or gen.DEFAULT_N[cfg]
+    flags = gen.FLAGS[cfg]
+    hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
+           for r in range(slots)]
+    dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
+    rec_bytes = REC16_BYTES if compact else REC_BYTES
+    recs = [torch.empty(hb.n * rec_bytes, dtype=torch.uint8, device="cuda") for hb in hbs]
+    ring = engine.ring_slots(dbs, recs, compact=compact)
+    stream = torch.cuda.current_stream()
+
+    def one():
+        engine.parse_ring(ring, flags, 0, stream=stream, compact=compact)
+    k, t_w = 0, time.perf_counter()
+    while k < args.warmup or time.perf_counter() - t_w < args.min_warmup_s:
+        one()
+        k += 1
+        if k % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    steps = max(4, args.steps // slots)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        one()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    frames = sum(hb.n for hb in hbs)
+    alg = sum(algorithmic_bytes(hb, rec_bytes=rec_bytes) for hb in hbs)
+    achieved = alg / (kern_ms / 1e3) / 1e9
+    out = {"mpps": frames * world * steps / wall / 1e6, "kernel_ms": kern_ms,
+           "ms_per_step": wall / steps * 1e3, "frames_per_launch": frames, "slots": slots,
+           "launches": steps, "record_bytes": rec_bytes, "flags": FLAG_NAMES[flags],
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "alg_bytes_per_launch": int(alg)},
+           "what": "rpkt_gpu_parse_ring%s: %d slots of %d frames in one launch" % (
+               "_compact" if compact else "", slots, n)}
+    del dbs, recs, ring
     torch.cuda.empty_cache()
     return out
 
@@ -853,8 +923,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 7])
-    ap.add_argument("--also", default="3,4,5,7", help="extra configs reported under 'extra'")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 7, 10, 11])
+    ap.add_argument("--also", default="3,4,5,7,10,11",
+                    help="extra configs reported under 'extra'")
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -885,6 +956,9 @@ def main():
     ap.add_argument("--strong", default="2,3",
                     help="configs also timed as one batch split over the ranks "
                          "(extra.config<N>_strong)")
+    ap.add_argument("--ring", default="2",
+                    help="configs also timed as 8 full batches per rpkt_gpu_parse_ring launch "
+                         "(extra.config<N>_ring8[_compact])")
     ap.add_argument("--opts", default="5",
                     help="configs also timed as the fused parse + option walks "
                          "(extra.config<N>_opts, extra.config<N>_opts_compact)")
@@ -928,7 +1002,7 @@ def main():
         args.cpu_threads = usable_cpus()
 
     main_res = run_config(args.config, args, rank, world, cpu=want_cpu and not args.main_opts,
-                          compact=args.record == "compact", opts=args.main_opts)
+                          compact=args.record == "compact", opts=args.main_opts, main=True)
     extra = {}
     for c in [int(x) for x in args.also.split(",") if x.strip()]:
         if c != args.config:
@@ -943,6 +1017,9 @@ def main():
         extra["config%d_opts" % c] = run_config(c, args, rank, world, opts=True)
         extra["config%d_opts_compact" % c] = run_config(c, args, rank, world, compact=True,
                                                         opts=True)
+    for c in [int(x) for x in args.ring.split(",") if x.strip()]:
+        extra["config%d_ring8" % c] = run_ring(c, args, rank, world)
+        extra["config%d_ring8_compact" % c] = run_ring(c, args, rank, world, compact=True)
     if world == 1 and args.host.strip():
         extra["host_inclusive"] = run_host(args)
     if world == 1 and args.rx_graph.strip():
@@ -951,7 +1028,7 @@ def main():
         extra["config1"] = run_config1(args)
 
     if rank == 0:
-        fb = {2: 64, 3: 1500, 7: 8000}.get(args.config)
+        fb = {2: 64, 3: 1500, 7: 8000, 10: 64, 11: 1500}.get(args.config)
         line = {
             "metric": METRIC,
             "value": round(main_res["mpps"], 2),

@@ -33,6 +33,12 @@ pub const RPKT_S_UDP_SHORT: u8 = 10;
 pub const RPKT_S_UDP_BAD_LEN: u8 = 11;
 pub const RPKT_S_TCP_SHORT: u8 = 12;
 pub const RPKT_S_TCP_BAD_DOFF: u8 = 13;
+pub const RPKT_S_IP6_SHORT: u8 = 14;
+pub const RPKT_S_IP6_BAD_LEN: u8 = 15;
+pub const RPKT_S_IP6_EXT_SHORT: u8 = 16;
+pub const RPKT_S_IP6_EXT_BAD_LEN: u8 = 17;
+pub const RPKT_S_IP6_FRAGMENT: u8 = 18;
+pub const RPKT_MAX_IP6_EXT: usize = 8;
 
 // enum rpkt_err
 pub const RPKT_OK: c_int = 0;
@@ -46,6 +52,7 @@ pub const RPKT_E_COLL: c_int = -5;
 pub const RPKT_F_IP_SUM: u32 = 1;
 pub const RPKT_F_L4_SUM: u32 = 2;
 pub const RPKT_F_FLOW_EV: u32 = 4;
+pub const RPKT_F_IPV6: u32 = 8;
 pub const RPKT_BUILD_IP_CSUM: u32 = 1;
 pub const RPKT_BUILD_L4_CSUM: u32 = 2;
 

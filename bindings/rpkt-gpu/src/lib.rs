@@ -18,7 +18,8 @@
 //! `parse` returns `Ok` exactly when the reference `parse` at that position returned
 //! `Ok` for the frame, and `Err(cursor)` (the cursor unchanged, as `ipv4/generated.rs:37,48`
 //! return the buffer) otherwise.  The same mapping is implemented and tested in Python
-//! (`rpkt_amd/views.py`, `tests/test_views.py`).
+//! (`rpkt_amd/views.py`, exercised by `tests/test_oracle_golden.py` and
+//! `tests/test_oracle_ip6.py`).
 pub mod ffi;
 
 use core::net::Ipv4Addr;
@@ -35,10 +36,11 @@ pub fn check(rc: i32) -> Result<(), Error> {
 
 /// The name of a per-frame status (`rpkt_gpu_status_name`).
 pub fn status_name(status: u8) -> &'static str {
-    const NAMES: [&str; 14] = ["OK", "ETH_SHORT", "VLAN_SHORT", "NOT_IPV4", "IP_SHORT",
+    const NAMES: [&str; 19] = ["OK", "ETH_SHORT", "VLAN_SHORT", "NOT_IPV4", "IP_SHORT",
                                "IP_BAD_IHL", "IP_IHL_GT_LEN", "IP_TOT_LT_IHL", "IP_TOT_GT_LEN",
                                "L4_OTHER", "UDP_SHORT", "UDP_BAD_LEN", "TCP_SHORT",
-                               "TCP_BAD_DOFF"];
+                               "TCP_BAD_DOFF", "IP6_SHORT", "IP6_BAD_LEN", "IP6_EXT_SHORT",
+                               "IP6_EXT_BAD_LEN", "IP6_FRAGMENT"];
     NAMES.get(status as usize).copied().unwrap_or("?")
 }
 
@@ -53,9 +55,15 @@ pub mod ether_type {
 
 /// rpkt/src/ipv4/mod.rs:107-155 (the values the path dispatches on).
 pub mod ip_protocol {
+    pub const IPV6_HOP_BY_HOP_OPTS: u8 = 0;
     pub const ICMP: u8 = 1;
     pub const TCP: u8 = 6;
     pub const UDP: u8 = 17;
+    pub const IPV6_ROUTE: u8 = 43;
+    pub const IPV6_FRAG: u8 = 44;
+    pub const AH: u8 = 51;
+    pub const ICMPV6: u8 = 58;
+    pub const IPV6_DEST_OPTS: u8 = 60;
 }
 
 #[derive(Clone, Copy, Debug, PartialEq, Eq)]
@@ -88,6 +96,13 @@ impl<'a> Cursor<'a> {
 const fn ip_failed(s: u8) -> bool {
     matches!(s, ffi::RPKT_S_ETH_SHORT | ffi::RPKT_S_VLAN_SHORT | ffi::RPKT_S_NOT_IPV4
                 | ffi::RPKT_S_IP_SHORT..=ffi::RPKT_S_IP_TOT_GT_LEN)
+}
+
+/// The record holds the IPv6 block (an RPKT_F_IPV6 parse dispatched it on 0x86DD).
+pub fn is_ip6(r: &Rec) -> bool {
+    let et = match r.n_vlan { 0 => r.ethertype, n => r.vlan_ethertype[(n - 1) as usize] };
+    et == ether_type::IPV6
+        && !matches!(r.status, ffi::RPKT_S_ETH_SHORT | ffi::RPKT_S_VLAN_SHORT | ffi::RPKT_S_NOT_IPV4)
 }
 
 /// EtherFrame (ether/generated.rs:17-67).
@@ -141,7 +156,7 @@ impl<'a> Ipv4<'a> {
     /// ipv4/generated.rs:35-51 (its five checks, in order, decided by the engine).
     pub fn parse(buf: Cursor<'a>) -> Result<Self, Cursor<'a>> {
         let r = buf.rec;
-        if buf.stage != Stage::L3 || buf.vlan_idx != r.n_vlan || ip_failed(r.status) {
+        if buf.stage != Stage::L3 || buf.vlan_idx != r.n_vlan || ip_failed(r.status) || is_ip6(r) {
             return Err(buf);
         }
         Ok(Ipv4 { buf })
@@ -172,6 +187,53 @@ impl<'a> Ipv4<'a> {
     }
 }
 
+/// Ipv6 (ipv6/generated.rs:22-216) over an IPv6 record: the record's IPv6 block
+/// (include/rpkt_gpu.h, bytes 24..43); the addresses are read from the frame.
+#[derive(Clone, Copy, Debug)]
+pub struct Ipv6<'a> { buf: Cursor<'a> }
+
+impl<'a> Ipv6<'a> {
+    /// ipv6/generated.rs:40-51: Err iff chunk_len < 40 or payload_len + 40 > remaining.
+    pub fn parse(buf: Cursor<'a>) -> Result<Self, Cursor<'a>> {
+        let r = buf.rec;
+        if buf.stage != Stage::L3 || buf.vlan_idx != r.n_vlan || !is_ip6(r)
+            || matches!(r.status, ffi::RPKT_S_IP6_SHORT | ffi::RPKT_S_IP6_BAD_LEN) {
+            return Err(buf);
+        }
+        Ok(Ipv6 { buf })
+    }
+    fn r(&self) -> &Rec { self.buf.rec }
+    fn vtcfl(&self) -> u32 {
+        self.r().ip_vhl as u32 | (self.r().ip_tos as u32) << 8 | (self.r().ip_packet_len as u32) << 16
+    }
+    pub fn version(&self) -> u8 { (self.vtcfl() >> 28) as u8 }
+    pub fn traffic_class(&self) -> u8 { (self.vtcfl() >> 20) as u8 }
+    pub fn flow_label(&self) -> u32 { self.vtcfl() & 0xfffff }
+    pub fn payload_len(&self) -> u16 { self.r().ip_ident }
+    pub fn next_header(&self) -> u8 { self.r().ip_frag as u8 }
+    pub fn hop_limit(&self) -> u8 { (self.r().ip_frag >> 8) as u8 }
+    /// Extension headers the engine walked before the upper-layer header.
+    pub fn n_ext(&self) -> u8 { self.r().ip_ttl }
+    /// The upper-layer protocol (the next_header where the extension walk stopped).
+    pub fn upper_protocol(&self) -> u8 { self.r().ip_protocol }
+    pub fn src_addr(&self, frame: &[u8]) -> core::net::Ipv6Addr {
+        let o = self.r().l3_off as usize + 8;
+        core::net::Ipv6Addr::from(<[u8; 16]>::try_from(&frame[o..o + 16]).unwrap())
+    }
+    pub fn dst_addr(&self, frame: &[u8]) -> core::net::Ipv6Addr {
+        let o = self.r().l3_off as usize + 24;
+        core::net::Ipv6Addr::from(<[u8; 16]>::try_from(&frame[o..o + 16]).unwrap())
+    }
+    /// The cursor past the extension headers (the upper-layer header, where Udp::parse /
+    /// Tcp::parse apply): the end of the reference loop over DestOptions::parse,
+    /// RoutingHeader::parse, ... and their payload().
+    pub fn upper_layer(self) -> Cursor<'a> {
+        let r = self.r();
+        let end = r.l3_off as u32 + 40 + self.payload_len() as u32;
+        Cursor { stage: Stage::L4, off: r.l4_off as u32, len: end - r.l4_off as u32, ..self.buf }
+    }
+}
+
 fn l4_parse<'a>(buf: Cursor<'a>, proto: u8) -> Result<Cursor<'a>, Cursor<'a>> {
     let r = buf.rec;
     if buf.stage != Stage::L4 || r.status != ffi::RPKT_S_OK || r.ip_protocol != proto {
@@ -195,8 +257,11 @@ impl<'a> Udp<'a> {
     pub fn packet_len(&self) -> u16 { self.buf.rec.l4_word6 }
     /// checksum::combine(&[pseudo_header, from_slice(udp)]) as the engine computed it.
     pub fn sum(&self) -> u16 { self.buf.rec.l4_sum }
-    /// smoltcp's policy (the origin of checksum.rs): a zero checksum is "not computed".
-    pub fn verify_checksum(&self) -> bool { self.checksum() == 0 || self.sum() == 0xffff }
+    /// smoltcp's policy (the origin of checksum.rs): a zero checksum is "not computed",
+    /// over IPv4 only (RFC 8200 section 8.1: mandatory over IPv6).
+    pub fn verify_checksum(&self) -> bool {
+        (self.checksum() == 0 && !is_ip6(self.buf.rec)) || self.sum() == 0xffff
+    }
     /// udp/generated.rs:66-76: advance 8, trimmed to packet_len.
     pub fn payload(self) -> Cursor<'a> {
         let r = self.buf.rec;
@@ -247,8 +312,10 @@ impl<'a> Tcp<'a> {
 impl Rec16 {
     pub fn parsed_ok(&self) -> bool { self.status == ffi::RPKT_S_OK }
     /// Ipv4::parse returned Ok (the header is at l3_off, the payload at l4_off).
-    pub fn ipv4_parsed(&self) -> bool { !ip_failed(self.status) }
+    pub fn ipv4_parsed(&self) -> bool { !ip_failed(self.status) && !self.is_ip6() }
     pub fn ip_sum_ok(&self) -> bool { self.verdict & 1 != 0 }
+    /// The frame was dispatched to Ipv6::parse (verdict bit 2).
+    pub fn is_ip6(&self) -> bool { self.verdict & 4 != 0 }
     /// status OK and the L4 sum verifies (a UDP checksum of 0 counts as verified).
     pub fn l4_sum_ok(&self) -> bool { self.verdict & 2 != 0 }
     /// (offset, length) of Udp::payload() / Tcp::payload() (status OK), else of

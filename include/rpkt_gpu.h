@@ -57,10 +57,24 @@ enum rpkt_status {
     RPKT_S_UDP_SHORT = 10,      /* chunk_len < 8      udp/generated.rs:33          */
     RPKT_S_UDP_BAD_LEN = 11,    /* len < 8 || len > remaining  udp/generated.rs:38 */
     RPKT_S_TCP_SHORT = 12,      /* chunk_len < 20     tcp/generated.rs:36          */
-    RPKT_S_TCP_BAD_DOFF = 13    /* hlen < 20 || hlen > chunk_len  tcp/generated.rs:41 */
+    RPKT_S_TCP_BAD_DOFF = 13,   /* hlen < 20 || hlen > chunk_len  tcp/generated.rs:41 */
+    /* IPv6 (RPKT_F_IPV6 only): ethertype 0x86DD -> Ipv6::parse -> extension headers */
+    RPKT_S_IP6_SHORT = 14,      /* chunk_len < 40     ipv6/generated.rs:42         */
+    RPKT_S_IP6_BAD_LEN = 15,    /* payload_len + 40 > remaining  ipv6/generated.rs:47 */
+    RPKT_S_IP6_EXT_SHORT = 16,  /* extension header: chunk_len < its fixed size
+                                   (2 HopByHop/DestOptions, 8 Routing/Fragment, 12 AH;
+                                   ipv6/generated.rs:243,386,530,698,852)          */
+    RPKT_S_IP6_EXT_BAD_LEN = 17,/* extension header: header_len < min or > chunk_len
+                                   (ipv6/generated.rs:248,391,535,857)             */
+    RPKT_S_IP6_FRAGMENT = 18    /* a Fragment header with offset != 0 or M set: the
+                                   upper-layer header needs reassembly, not parsed */
 };
 
 #define RPKT_MAX_VLAN 2
+/* Extension headers walked after the IPv6 header: HopByHop (0), Routing (43),
+ * Fragment (44), DestOptions (60), AH (51).  A chain longer than this leaves the next
+ * header at an extension type -> RPKT_S_L4_OTHER (as a third VLAN tag -> NOT_IPV4). */
+#define RPKT_MAX_IP6_EXT 8
 
 /* ---- API return codes ---- */
 enum rpkt_err {
@@ -76,7 +90,9 @@ enum rpkt_err {
 enum rpkt_flags {
     RPKT_F_IP_SUM = 1u,      /* compute ip_sum = from_slice(ipv4 header[0..ihl4])  */
     RPKT_F_L4_SUM = 2u,      /* compute l4_sum = combine(pseudo, from_slice(l4))    */
-    RPKT_F_FLOW_EV = 4u      /* also write one rpkt_flow_ev_t per frame             */
+    RPKT_F_FLOW_EV = 4u,     /* also write one rpkt_flow_ev_t per frame             */
+    RPKT_F_IPV6 = 8u         /* also decode and verify IPv6 (ethertype 0x86DD); without
+                                it such frames stop at RPKT_S_NOT_IPV4 as before      */
 };
 
 /* Record layout: 80 bytes, 16-byte aligned, little-endian host order.
@@ -103,7 +119,37 @@ enum rpkt_flags {
  *   l4_sum             checksum::combine(&[pseudo(src,dst,proto,l4_len),
  *                      from_slice(l4[0..l4_len])]); 0xffff <=> valid
  * Fields of layers that were not reached are zero.  Sums not requested by the
- * flags, or whose layer did not parse, are zero. */
+ * flags, or whose layer did not parse, are zero.
+ *
+ * IPv6 frames (RPKT_F_IPV6, dispatch ethertype 0x86DD: `ethertype`, or
+ * vlan_ethertype[n_vlan-1] when tagged) use bytes 24..43 as the IPv6 block below
+ * instead of the IPv4 fields; everything else keeps its meaning.  Chain:
+ * Ipv6::parse (ipv6/generated.rs:40-51) -> Ipv6::payload (trim to payload_len,
+ * advance 40, :83-92) -> up to RPKT_MAX_IP6_EXT extension headers, each its parse and
+ * payload() (DestOptions :241-279, HopByHopOption :384-421, RoutingHeader :528-577,
+ * FragmentHeader :696-739, AuthenticationHeader :850-899) -> Udp|Tcp::parse.
+ *   24 u32 ip6_vtcfl     be32 of bytes 0..3: version = >>28, traffic_class =
+ *                        (>>20)&0xff, flow_label = &0xfffff     (:57-67)
+ *   28 u16 ip6_payload_len                                      (:77-79)
+ *   30 u8  ip6_next_header   the IPv6 header's next_header       (:69-71)
+ *   31 u8  ip6_hop_limit                                         (:73-75)
+ *   32 u8  ip6_n_ext     extension headers walked
+ *   33 u8  ip_protocol   the upper-layer protocol: the next_header where the walk
+ *                        stopped (the extension type that failed for IP6_EXT_*,
+ *                        the Fragment header's next_header for IP6_FRAGMENT)
+ *   34 u16 ip6_pdst_off  frame offset of the 16-B address the L4 pseudo header uses
+ *                        as destination: dst_addr (l3 + 24), or, after a Routing
+ *                        header with segments_left > 0 (RFC 8200 section 8.1), its
+ *                        final address -- the last of the list for types 0 and 2, the
+ *                        first (Segment List[0]) for type 4; other types keep dst_addr
+ *   36 u32 ip6_src_fold  src_addr as four be32 words XORed (the flow key)
+ *   40 u32 ip6_dst_fold  dst_addr likewise (src_addr/dst_addr themselves: frame bytes
+ *                        l3_off + 8 and l3_off + 24, or rpkt_gpu_fields_batch)
+ * l4_off = the cursor after the extension headers (the header where the walk stopped);
+ * payload_off/_len = Udp/Tcp::payload() when status == OK, otherwise [l4_off, end of
+ * the trimmed IPv6 payload).  ip_sum = 0 (IPv6 has no header checksum).  l4_sum =
+ * combine(&[pseudo_v6(src, pdst, u32 l4_len, next header), from_slice(l4)]); a UDP
+ * checksum of 0 is NOT "not computed" over IPv6 (RFC 8200 section 8.1). */
 typedef struct rpkt_rec {
     uint8_t  status;            /*  0 enum rpkt_status                          */
     uint8_t  n_vlan;            /*  1 tags walked, 0..RPKT_MAX_VLAN             */
@@ -145,8 +191,9 @@ typedef struct rpkt_rec {
  *   bits  0..31  frame_len
  *   bits 32..47  flow bucket = rpkt_flow_hash(5-tuple) % n_buckets (status OK),
  *                n_buckets for frames that did not parse to L4
- *   bit  48      ip header sum != 0xffff
- *   bit  49      l4 sum != 0xffff (a UDP checksum field of 0 counts as valid)
+ *   bit  48      ip header sum != 0xffff (IPv4 header parsed; never for IPv6)
+ *   bit  49      l4 sum != 0xffff (an IPv4 UDP checksum field of 0 counts as valid)
+ * IPv6 frames hash ip6_src_fold / ip6_dst_fold in place of the IPv4 addresses.
  * Counters (rpkt_gpu_flow_count) are u64[(n_buckets + 1) * 4]:
  *   row b = {pkts, bytes, ip_bad, l4_bad}; row n_buckets = unparsed frames. */
 typedef uint64_t rpkt_flow_ev_t;
@@ -190,9 +237,10 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* batch, uint32_t flags,
  * layers and read the verdicts, for receive loops that read getters from the frame
  * itself (rpkt's views hold only the buffer and read fields lazily,
  * ipv4/generated.rs:17-20).  Fields equal the rpkt_rec_t fields of the same name;
- * verdict bit 0 = RPKT_F_IP_SUM requested and ip_sum == 0xffff, bit 1 =
- * RPKT_F_L4_SUM requested, status OK and (l4_sum == 0xffff or a UDP checksum field
- * of 0: "not computed"). */
+ * verdict bit 0 = RPKT_F_IP_SUM requested and ip_sum == 0xffff (IPv6: requested and
+ * the IPv6 header parsed -- it carries no checksum), bit 1 = RPKT_F_L4_SUM requested,
+ * status OK and (l4_sum == 0xffff or, IPv4 only, a UDP checksum field of 0: "not
+ * computed"), bit 2 = the frame was dispatched to Ipv6::parse (RPKT_F_IPV6). */
 typedef struct rpkt_rec16 {
     uint8_t  status;            /*  0 enum rpkt_status                          */
     uint8_t  n_vlan;            /*  1                                           */

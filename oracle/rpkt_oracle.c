@@ -142,9 +142,182 @@ uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8
     return oracle_combine(parts, 3);
 }
 
+/* smoltcp pseudo_header_v6 (the same origin; RFC 8200 section 8.1):
+ * combine(&[data(src), data(dst), data(&(length as u32).to_be_bytes()),
+ * data(&[0, 0, 0, next_header])]). */
+uint16_t oracle_pseudo_header_v6(const uint8_t* src16, const uint8_t* dst16, uint8_t proto,
+                                 uint32_t length) {
+    uint8_t len_be[4] = {(uint8_t)(length >> 24), (uint8_t)(length >> 16), (uint8_t)(length >> 8),
+                         (uint8_t)length};
+    uint8_t nh[4] = {0, 0, 0, proto};
+    uint16_t parts[4] = {oracle_from_slice(src16, 16), oracle_from_slice(dst16, 16),
+                         oracle_from_slice(len_be, 4), oracle_from_slice(nh, 4)};
+    return oracle_combine(parts, 4);
+}
+
 /* ------------------------------------------------------------------------- */
 /* The decode chain for one frame                                             */
 /* ------------------------------------------------------------------------- */
+
+/* Udp::parse / Tcp::parse on the cursor the IP layer's payload() returned, getters,
+ * the L4 sum with the pseudo header of the IP version (addresses src/dst, 4 or 16
+ * bytes) and payload().  Shared by the IPv4 and IPv6 chains. */
+static void oracle_parse_l4(cursor_t* buf, uint8_t proto, const uint8_t* src, const uint8_t* dst,
+                            int v6, uint32_t flags, rpkt_rec_t* rec) {
+    if (proto == 17) {
+        /* Udp::parse, udp/generated.rs:31-42 */
+        if (cur_remaining(buf) < 8) { rec->status = RPKT_S_UDP_SHORT; return; }
+        const uint8_t* u = cur_chunk(buf);
+        size_t ulen = be16(u + 4);                    /* packet_len :59-62 */
+        if (ulen < 8 || ulen > cur_remaining(buf)) { rec->status = RPKT_S_UDP_BAD_LEN; return; }
+        rec->src_port = be16(u);                      /* :48-51 */
+        rec->dst_port = be16(u + 2);                  /* :52-55 */
+        rec->l4_word6 = (uint16_t)ulen;
+        rec->l4_checksum = be16(u + 6);               /* :56-58 */
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {v6 ? oracle_pseudo_header_v6(src, dst, 17, (uint32_t)ulen)
+                                    : oracle_pseudo_header_v4(src, dst, 17, (uint16_t)ulen),
+                                 oracle_from_slice(u, ulen)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        /* Udp::payload, udp/generated.rs:66-76: trim to len, advance 8 */
+        size_t ts = cur_remaining(buf) - ulen;
+        if (ts > 0) cur_trim_off(buf, ts);
+        cur_advance(buf, 8);
+        rec->payload_off = (uint16_t)buf->start;
+        rec->payload_len = (uint16_t)cur_remaining(buf);
+        rec->status = RPKT_S_OK;
+    } else if (proto == 6) {
+        /* Tcp::parse, tcp/generated.rs:34-45 */
+        size_t cl = cur_remaining(buf);
+        if (cl < 20) { rec->status = RPKT_S_TCP_SHORT; return; }
+        const uint8_t* t = cur_chunk(buf);
+        size_t hl = (size_t)(t[12] >> 4) * 4;         /* header_len :119-121 */
+        if (hl < 20 || hl > cl) { rec->status = RPKT_S_TCP_BAD_DOFF; return; }
+        rec->src_port = be16(t);                      /* :55-62 */
+        rec->dst_port = be16(t + 2);
+        rec->tcp_seq = be32(t + 4);                   /* :63-66 */
+        rec->tcp_ack = be32(t + 8);                   /* :67-70 */
+        rec->l4_word6 = be16(t + 12);                 /* header_len/reserved/flags :71-106 */
+        rec->tcp_window = be16(t + 14);               /* :107-110 */
+        rec->l4_checksum = be16(t + 16);              /* :111-114 */
+        rec->tcp_urgent = be16(t + 18);               /* :115-118 */
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {v6 ? oracle_pseudo_header_v6(src, dst, 6, (uint32_t)cl)
+                                    : oracle_pseudo_header_v4(src, dst, 6, (uint16_t)cl),
+                                 oracle_from_slice(t, cl)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        cur_advance(buf, hl);                         /* Tcp::payload :125-131 (no trim) */
+        rec->payload_off = (uint16_t)buf->start;
+        rec->payload_len = (uint16_t)cur_remaining(buf);
+        rec->status = RPKT_S_OK;
+    } else {
+        rec->status = RPKT_S_L4_OTHER;
+    }
+}
+
+static uint32_t fold_be32x4(const uint8_t* a) {
+    return be32(a) ^ be32(a + 4) ^ be32(a + 8) ^ be32(a + 12);
+}
+
+/* The IPv6 chain from the cursor at the IPv6 header (RPKT_F_IPV6; include/rpkt_gpu.h
+ * documents the record's IPv6 block).  Ipv6::parse ipv6/generated.rs:40-51, getters
+ * :57-80 and :194-205, Ipv6::payload :83-92; then the extension headers a receive loop
+ * steps through (ipv6_test.rs:27-76, 137-178, 233-269, 327-352, 397-421): each is the
+ * generated parse of its type and payload() = advance(header_len), until the next
+ * header is not an extension type. */
+static void oracle_parse_ip6(cursor_t* buf, uint32_t flags, rpkt_rec_t* rec) {
+    rec->l3_off = (uint16_t)buf->start;
+    size_t chunk_len = cur_remaining(buf);
+    if (chunk_len < 40) { rec->status = RPKT_S_IP6_SHORT; return; }          /* :42 */
+    const uint8_t* ip = cur_chunk(buf);
+    size_t payload_len = be16(ip + 4);                                        /* :77-79 */
+    if (payload_len + 40 > cur_remaining(buf)) { rec->status = RPKT_S_IP6_BAD_LEN; return; } /* :47 */
+    /* record block: ip_vhl..ip_dst reinterpreted (rpkt_rec_t bytes 24..43) */
+    uint8_t* blk = (uint8_t*)rec + 24;
+    uint32_t vtcfl = be32(ip);                       /* version :57-59, traffic_class :61-63,
+                                                        flow_label :65-67 */
+    uint16_t pl = (uint16_t)payload_len;
+    uint16_t pdst_off = (uint16_t)(buf->start + 24);
+    uint32_t sf = fold_be32x4(ip + 8), df = fold_be32x4(ip + 24);   /* src/dst :196-204 */
+    memcpy(blk + 0, &vtcfl, 4);
+    memcpy(blk + 4, &pl, 2);
+    blk[6] = ip[6];                                  /* next_header :69-71 */
+    blk[7] = ip[7];                                  /* hop_limit :73-75 */
+    memcpy(blk + 12, &sf, 4);
+    memcpy(blk + 16, &df, 4);
+    const uint8_t* pdst = ip + 24;
+
+    /* Ipv6::payload, :83-92: trim to 40 + payload_len, advance 40 */
+    size_t trim_size = cur_remaining(buf) - (40 + payload_len);
+    if (trim_size > 0) cur_trim_off(buf, trim_size);
+    cur_advance(buf, 40);
+
+    uint8_t nh = ip[6];
+    uint8_t n_ext = 0;
+    int stop = 0;
+    for (; n_ext < RPKT_MAX_IP6_EXT; n_ext++) {
+        size_t cl = cur_remaining(buf);
+        const uint8_t* h = cur_chunk(buf);
+        size_t hl;
+        if (nh == 0 || nh == 60) {
+            /* HopByHopOption::parse :384-395 / DestOptions::parse :241-252:
+             * chunk_len >= 2, header_len = b1 * 8 + 8 (:410-412, :267-269) <= chunk_len */
+            if (cl < 2) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (size_t)h[1] * 8 + 8;
+            if (hl < 2 || hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        } else if (nh == 43) {
+            /* RoutingHeader::parse :528-539, header_len :566-568 */
+            if (cl < 8) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (size_t)h[1] * 8 + 8;
+            if (hl < 8 || hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+            /* segments_left :558-560 > 0: the pseudo header's destination is the final
+             * address (RFC 8200 section 8.1); type_ :554-556 */
+            if (h[3] > 0) {
+                size_t n_addr = (hl - 8) / 16;
+                if (h[2] == 4 && n_addr >= 1) pdst = h + 8;                        /* SRH */
+                else if ((h[2] == 0 || h[2] == 2) && n_addr >= 1) pdst = h + 8 + 16 * (n_addr - 1);
+                if (pdst != ip + 24) pdst_off = (uint16_t)(buf->start + (size_t)(pdst - h));
+            }
+        } else if (nh == 44) {
+            /* FragmentHeader::parse :696-703 (chunk_len >= 8), offset :717-719,
+             * more_frag :725-727, payload :735-739 (advance 8) */
+            if (cl < 8) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = 8;
+            uint16_t off = (uint16_t)(be16(h + 2) >> 3);
+            int more = h[3] & 1;
+            if (off != 0 || more) {
+                nh = h[0];
+                cur_advance(buf, hl);
+                n_ext++;
+                stop = RPKT_S_IP6_FRAGMENT;
+                break;
+            }
+        } else if (nh == 51) {
+            /* AuthenticationHeader::parse :850-861, header_len = b1 * 4 + 8 :888-890 */
+            if (cl < 12) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (size_t)h[1] * 4 + 8;
+            if (hl < 12 || hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        } else {
+            break;                                   /* the upper-layer header */
+        }
+        nh = h[0];                                   /* next_header of every type */
+        cur_advance(buf, hl);                        /* payload(): advance(header_len) */
+    }
+    blk[8] = n_ext;
+    blk[9] = nh;                                     /* ip_protocol */
+    memcpy(blk + 10, &pdst_off, 2);
+    rec->l4_off = (uint16_t)buf->start;
+    rec->payload_off = (uint16_t)buf->start;
+    rec->payload_len = (uint16_t)cur_remaining(buf);
+    if (stop) { rec->status = (uint8_t)stop; return; }
+    if (nh == 0 || nh == 43 || nh == 44 || nh == 60 || nh == 51) {
+        rec->status = RPKT_S_L4_OTHER;               /* RPKT_MAX_IP6_EXT reached */
+        return;
+    }
+    oracle_parse_l4(buf, nh, ip + 8, pdst, 1, flags, rec);
+}
 
 /* Parse one frame exactly as the reference chain would, filling `rec`.
  * Chain: benches/rpkt/rpkt_parse.rs:62-80 (Ether -> IPv4 -> UDP) generalised
@@ -176,6 +349,10 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
         rec->vlan_ethertype[rec->n_vlan] = et;
         rec->n_vlan++;
         cur_advance(&buf, 4);
+    }
+    if (et == 0x86dd && (flags & RPKT_F_IPV6)) {     /* EtherType::IPV6, ipv6_test.rs:25 */
+        oracle_parse_ip6(&buf, flags, rec);
+        return;
     }
     if (et != 0x0800) { rec->status = RPKT_S_NOT_IPV4; return; }   /* rpkt_parse.rs:66 */
 
@@ -212,56 +389,22 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
     rec->payload_off = (uint16_t)buf.start;
     rec->payload_len = (uint16_t)cur_remaining(&buf);
 
-    uint8_t proto = ip[9];
-    if (proto == 17) {
-        /* Udp::parse, udp/generated.rs:31-42 */
-        if (cur_remaining(&buf) < 8) { rec->status = RPKT_S_UDP_SHORT; return; }
-        const uint8_t* u = cur_chunk(&buf);
-        size_t ulen = be16(u + 4);                    /* packet_len :59-62 */
-        if (ulen < 8 || ulen > cur_remaining(&buf)) { rec->status = RPKT_S_UDP_BAD_LEN; return; }
-        rec->src_port = be16(u);                      /* :48-51 */
-        rec->dst_port = be16(u + 2);                  /* :52-55 */
-        rec->l4_word6 = (uint16_t)ulen;
-        rec->l4_checksum = be16(u + 6);               /* :56-58 */
-        if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 17, (uint16_t)ulen),
-                                 oracle_from_slice(u, ulen)};
-            rec->l4_sum = oracle_combine(parts, 2);
-        }
-        /* Udp::payload, udp/generated.rs:66-76: trim to len, advance 8 */
-        size_t ts = cur_remaining(&buf) - ulen;
-        if (ts > 0) cur_trim_off(&buf, ts);
-        cur_advance(&buf, 8);
-        rec->payload_off = (uint16_t)buf.start;
-        rec->payload_len = (uint16_t)cur_remaining(&buf);
-        rec->status = RPKT_S_OK;
-    } else if (proto == 6) {
-        /* Tcp::parse, tcp/generated.rs:34-45 */
-        size_t cl = cur_remaining(&buf);
-        if (cl < 20) { rec->status = RPKT_S_TCP_SHORT; return; }
-        const uint8_t* t = cur_chunk(&buf);
-        size_t hl = (size_t)(t[12] >> 4) * 4;         /* header_len :119-121 */
-        if (hl < 20 || hl > cl) { rec->status = RPKT_S_TCP_BAD_DOFF; return; }
-        rec->src_port = be16(t);                      /* :55-62 */
-        rec->dst_port = be16(t + 2);
-        rec->tcp_seq = be32(t + 4);                   /* :63-66 */
-        rec->tcp_ack = be32(t + 8);                   /* :67-70 */
-        rec->l4_word6 = be16(t + 12);                 /* header_len/reserved/flags :71-106 */
-        rec->tcp_window = be16(t + 14);               /* :107-110 */
-        rec->l4_checksum = be16(t + 16);              /* :111-114 */
-        rec->tcp_urgent = be16(t + 18);               /* :115-118 */
-        if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 6, (uint16_t)cl),
-                                 oracle_from_slice(t, cl)};
-            rec->l4_sum = oracle_combine(parts, 2);
-        }
-        cur_advance(&buf, hl);                        /* Tcp::payload :125-131 (no trim) */
-        rec->payload_off = (uint16_t)buf.start;
-        rec->payload_len = (uint16_t)cur_remaining(&buf);
-        rec->status = RPKT_S_OK;
-    } else {
-        rec->status = RPKT_S_L4_OTHER;
-    }
+    oracle_parse_l4(&buf, ip[9], ip + 12, ip + 16, 0, flags, rec);
+}
+
+/* The dispatch ethertype (the one Ipv4/Ipv6::parse was chosen on) and whether the
+ * record is an IPv6 record (include/rpkt_gpu.h: the IPv6 block). */
+static uint16_t rec_dispatch_et(const rpkt_rec_t* r) {
+    return r->n_vlan ? r->vlan_ethertype[r->n_vlan - 1] : r->ethertype;
+}
+int oracle_rec_is_ip6(const rpkt_rec_t* r) {
+    return r->status != RPKT_S_ETH_SHORT && r->status != RPKT_S_VLAN_SHORT &&
+           r->status != RPKT_S_NOT_IPV4 && rec_dispatch_et(r) == 0x86dd;
+}
+/* IPv4 header parsed (its sum and fields are valid) */
+int oracle_rec_ip4_parsed(const rpkt_rec_t* r) {
+    return !oracle_rec_is_ip6(r) &&
+           (r->status == RPKT_S_OK || (r->status >= RPKT_S_L4_OTHER && r->status <= RPKT_S_TCP_BAD_DOFF));
 }
 
 /* 5-tuple flow hash (shared definition with the device: include/rpkt_gpu.h). */
@@ -284,14 +427,15 @@ uint32_t oracle_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_
 uint64_t oracle_flow_event(const rpkt_rec_t* r, uint32_t n_buckets) {
     uint64_t ev = r->frame_len;
     uint32_t bucket = n_buckets;
-    int ip_parsed = r->status == RPKT_S_OK || r->status >= RPKT_S_L4_OTHER;
+    const int v6 = oracle_rec_is_ip6(r);
+    /* ip_src / ip_dst hold ip6_src_fold / ip6_dst_fold in an IPv6 record */
     if (r->status == RPKT_S_OK)
         bucket = oracle_flow_hash(r->ip_src, r->ip_dst, r->src_port, r->dst_port,
                                   r->ip_protocol) % n_buckets;
     ev |= (uint64_t)bucket << 32;
-    if (ip_parsed && r->ip_sum != 0xffff) ev |= 1ull << 48;
+    if (oracle_rec_ip4_parsed(r) && r->ip_sum != 0xffff) ev |= 1ull << 48;
     if (r->status == RPKT_S_OK && r->l4_sum != 0xffff &&
-        !(r->ip_protocol == 17 && r->l4_checksum == 0))
+        !(!v6 && r->ip_protocol == 17 && r->l4_checksum == 0))
         ev |= 1ull << 49;
     return ev;
 }

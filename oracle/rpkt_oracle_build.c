@@ -31,6 +31,7 @@
 #include "../include/rpkt_gpu.h"
 
 uint16_t oracle_from_slice(const uint8_t* data, size_t len);
+int oracle_rec_is_ip6(const rpkt_rec_t* r);
 uint16_t oracle_combine(const uint16_t* checksums, size_t n);
 uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
                                  uint16_t length);
@@ -53,6 +54,7 @@ static const uint8_t ETHER_T[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x
 int oracle_build_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t flags) {
     uint32_t nv = r->n_vlan;
     if (nv > RPKT_MAX_VLAN) return 0;
+    if (oracle_rec_is_ip6(r)) return 0;              /* the build writes IPv4 headers only */
     uint32_t l3 = 14 + 4 * nv;
     uint32_t ihl4 = (uint32_t)(r->ip_vhl & 0xf) * 4;
     uint32_t l4 = l3 + ihl4;

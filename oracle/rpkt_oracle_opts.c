@@ -20,6 +20,8 @@
 
 #include "../include/rpkt_gpu.h"
 
+int oracle_rec_ip4_parsed(const rpkt_rec_t* r);   /* rpkt_oracle.c */
+
 static uint16_t be16(const uint8_t* p) { return (uint16_t)(((uint16_t)p[0] << 8) | p[1]); }
 static uint32_t be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
@@ -60,8 +62,9 @@ static int ip_opt(const uint8_t* b, uint32_t n, int* kind) {
 void oracle_options_one(const uint8_t* f, uint32_t len, const rpkt_rec_t* r, rpkt_opts_t* o) {
     memset(o, 0, sizeof(*o));
     (void)len;
-    int ip_parsed = r->status == RPKT_S_OK || r->status >= RPKT_S_L4_OTHER;
-    if (ip_parsed) {
+    /* Ipv4OptionsIter runs over IPv4 headers only; TcpOptionsIter over any TCP header,
+     * behind IPv4 or IPv6 (rpkt_oracle.c) */
+    if (oracle_rec_ip4_parsed(r)) {
         const uint8_t* b = f + r->l3_off + 20;            /* var_header_slice :41-44 */
         uint32_t n = (uint32_t)(r->l4_off - r->l3_off - 20), pos = 0;
         o->ip_stop = RPKT_OPT_END;

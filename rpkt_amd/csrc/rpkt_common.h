@@ -549,6 +549,7 @@ struct LaneRec {
     uint32_t l4_part;                // in-window part of the L4 word sum
     uint32_t l4_start_abs, pseudo;
     bool want_l4;
+    bool is6;                        // dispatched to Ipv6::parse (RPKT_F_IPV6): the IPv6 block
 };
 
 // Window loads of one tile into registers: chunk c = k*64 + lane is piece c%8 of
@@ -660,11 +661,119 @@ __device__ __forceinline__ uint32_t raw_range_sum(const uint8_t* slot, const uin
 
 __device__ __forceinline__ bool is_tag(uint32_t et) { return et == 0x8100u || et == 0x88a8u; }
 
+// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout),
+// byte loads: the rare paths whose header lies outside the LDS window
+__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t (&F)[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        F[k] = gbyte(rs, a + 4 * k) | (gbyte(rs, a + 4 * k + 1) << 8) |
+               (gbyte(rs, a + 4 * k + 2) << 16) | (gbyte(rs, a + 4 * k + 3) << 24);
+}
+
+// Frame bytes x..x+3 of a lane's frame as a little-endian dword: from its LDS window
+// slot when they lie in the window, else byte-wise from global memory (IPv6 extension
+// headers past the window; bytes past the buffer read as 0).
+struct FrameDw {
+    const uint8_t* slot;
+    uint32_t ph, off;
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ uint32_t operator()(uint32_t x) const {
+        if (__builtin_expect(ph + x + 4u <= (uint32_t)kWin, 1)) {
+            const uint32_t y = ph + x, a = y & ~3u;
+            return align_bytes(lds32(slot, a + 4), lds32(slot, a), y & 3u);
+        }
+        const uint32_t g = off + x;
+        return gbyte(rs, g) | (gbyte(rs, g + 1) << 8) | (gbyte(rs, g + 2) << 16) |
+               (gbyte(rs, g + 3) << 24);
+    }
+};
+
+// RFC 1071 word sum of a 16-byte address given as frame-relative LE dwords: the four
+// host-order words' 16-bit halves (big-endian words, as the pseudo header sums them)
+__device__ __forceinline__ uint32_t addr_words_sum(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return halves(bswap32(a)) + halves(bswap32(b)) + halves(bswap32(c)) + halves(bswap32(d));
+}
+
+__device__ __forceinline__ bool is_ip6_ext(uint32_t nh) {
+    return nh == 0u || nh == 43u || nh == 44u || nh == 60u || nh == 51u;
+}
+
+// The IPv6 part of the parse (RPKT_F_IPV6, include/rpkt_gpu.h documents the record's
+// IPv6 block): Ipv6::parse (ipv6/generated.rs:40-51) and getters (:57-80, 194-205),
+// Ipv6::payload (:83-92: trim to 40 + payload_len, advance 40), then the extension
+// headers: each type's generated parse (DestOptions :241-252, HopByHopOption :384-395,
+// RoutingHeader :528-539, FragmentHeader :696-703, AuthenticationHeader :850-861) and
+// payload() = advance(header_len).  The 40-byte header always lies in the window (it
+// ends by frame byte 62); extension headers past it are read from global memory.
+// Returns the status; on OK: l4 (frame offset of the upper-layer header), its
+// remaining bytes, the protocol and the pseudo header's address sum.
+__device__ __forceinline__ uint32_t parse_ip6(const uint8_t* slot, uint32_t ph, Frame fr,
+                                              __amdgpu_buffer_rsrc_t rs, uint32_t l3, uint32_t rem,
+                                              uint32_t* w, uint32_t& l4, uint32_t& l4rem,
+                                              uint32_t& proto, uint32_t& paddr) {
+    if (rem < 40u) return RPKT_S_IP6_SHORT;                               // :42
+    uint32_t F[10];
+    {
+        const uint32_t x = ph + l3, a0 = x & ~3u, sh = x & 3u;
+        uint32_t R[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) R[k] = lds32(slot, a0 + 4 * k);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) F[k] = align_bytes(R[k + 1], R[k], sh);
+    }
+    const uint32_t plen = be16_lo(F[1]);                                  // payload_len :77-79
+    if (plen + 40u > rem) return RPKT_S_IP6_BAD_LEN;                      // :47
+    w[6] = bswap32(F[0]);                                                 // version, tc, flow
+    w[7] = plen | (F[1] & 0xffff0000u);                                   // next_header, hop_limit
+    w[9] = bswap32(F[2]) ^ bswap32(F[3]) ^ bswap32(F[4]) ^ bswap32(F[5]);    // src fold
+    w[10] = bswap32(F[6]) ^ bswap32(F[7]) ^ bswap32(F[8]) ^ bswap32(F[9]);   // dst fold
+    const uint32_t src_sum = addr_words_sum(F[2], F[3], F[4], F[5]);
+    uint32_t pdst_sum = addr_words_sum(F[6], F[7], F[8], F[9]);
+    uint32_t pdst_off = l3 + 24u;
+    const FrameDw dw{slot, ph, fr.off, rs};
+    uint32_t c = l3 + 40u;
+    const uint32_t end = c + plen;
+    uint32_t nh = (F[1] >> 16) & 0xffu, n_ext = 0, status = RPKT_S_OK;
+    for (int k = 0; k < RPKT_MAX_IP6_EXT && is_ip6_ext(nh); ++k) {
+        const bool fg = nh == 44u, ah = nh == 51u, rt = nh == 43u;
+        const uint32_t fixed = (nh == 0u || nh == 60u) ? 2u : (ah ? 12u : 8u);
+        const uint32_t cl = end - c;                                      // chunk_len
+        if (cl < fixed) { status = RPKT_S_IP6_EXT_SHORT; break; }
+        const uint32_t d0 = dw(c);                 // next_header, len, (type, segments_left)
+        const uint32_t b1 = (d0 >> 8) & 0xffu;
+        const uint32_t hl = fg ? 8u : (ah ? b1 * 4u + 8u : b1 * 8u + 8u);    // header_len
+        if (!fg && (hl < fixed || hl > cl)) { status = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        if (rt && (d0 >> 24) != 0u) {
+            // segments_left > 0: the pseudo header's destination is the final address
+            // (RFC 8200 section 8.1): the last of the list (types 0, 2), Segment List[0] (4)
+            const uint32_t type = (d0 >> 16) & 0xffu, n_addr = (hl - 8u) >> 4;
+            if (n_addr != 0u && (type == 0u || type == 2u || type == 4u)) {
+                const uint32_t a = c + 8u + (type == 4u ? 0u : 16u * (n_addr - 1u));
+                pdst_off = a;
+                pdst_sum = addr_words_sum(dw(a), dw(a + 4u), dw(a + 8u), dw(a + 12u));
+            }
+        }
+        nh = d0 & 0xffu;
+        c += hl;
+        n_ext += 1u;
+        // offset (:717-719) != 0 or more_frag (:725-727): a fragment, not reassembled here
+        if (fg && (be16_hi(d0) & 0xfff9u) != 0u) { status = RPKT_S_IP6_FRAGMENT; break; }
+    }
+    if (status == RPKT_S_OK && is_ip6_ext(nh)) status = RPKT_S_L4_OTHER;   // chain too long
+    w[8] = n_ext | (nh << 8) | (pdst_off << 16);
+    l4 = c;
+    l4rem = end - c;
+    proto = nh;
+    paddr = src_sum + pdst_sum;
+    return status;
+}
+
 // Lane-per-frame parse from the LDS window: the rpkt chain with every getter, the
 // IPv4 header sum and the in-window part of the L4 sum.  Three dependent rounds of
 // LDS dword reads: link layer (bytes 0..23), IPv4 header at l3, L4 header at l4.
 __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame fr, bool valid,
-                                           uint32_t flags, LaneRec& L) {
+                                           uint32_t flags, LaneRec& L,
+                                           __amdgpu_buffer_rsrc_t rs) {
     const uint32_t ph = fr.off & 15u;
     const uint8_t* slot = &W.win[lane * kSlot];
     uint32_t* w = L.w;
@@ -673,6 +782,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     const uint32_t len = valid ? fr.len : 0u;
     L.stream_s = L.stream_e = L.l4_part = L.l4_start_abs = L.pseudo = 0;
     L.want_l4 = false;
+    L.is6 = false;
     w[19] = len;
     uint32_t status = RPKT_S_OK;
 
@@ -718,48 +828,72 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
         }
     }
     w[0] = (nvlan << 8) | (eth_et << 16);
-    if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+    // EtherType::IPV6 (ether/mod.rs), ipv6_test.rs:25: with RPKT_F_IPV6 only
+    const bool v6 = (flags & RPKT_F_IPV6) && status == RPKT_S_OK && et == 0x86ddu;
+    if (status == RPKT_S_OK && et != 0x0800u && !v6) status = RPKT_S_NOT_IPV4;
     if (status != RPKT_S_OK) {
         w[0] |= status;
         L.status = status;
         return;
     }
 
-    // round 2: Ipv4::parse (ipv4/generated.rs:35-51) and getters (:61-112, 269-288)
     const uint32_t l3 = 14u + 4u * nvlan, rem = len - l3;
     w[16] = l3;
-    Hdr6 ip;
-    read_hdr(slot, ph + l3, ip);
-    const uint32_t vhl = ip.F[0] & 0xffu;
-    const uint32_t ihl4 = (vhl & 0xfu) * 4u;
-    const uint32_t tot = be16_hi(ip.F[0]);
-    if (rem < 20) status = RPKT_S_IP_SHORT;
-    else if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
-    else if (ihl4 > rem) status = RPKT_S_IP_IHL_GT_LEN;
-    else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
-    else if (tot > rem) status = RPKT_S_IP_TOT_GT_LEN;
-    if (status != RPKT_S_OK) {
-        w[0] |= status;
-        L.status = status;
-        return;
+    uint32_t l4, l4rem, proto, paddr;
+    if (v6) {
+        // round 2 (IPv6): the header, the extension headers, the pseudo header's addresses
+        L.is6 = true;
+        status = parse_ip6(slot, ph, fr, rs, l3, rem, w, l4, l4rem, proto, paddr);
+        if (status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN) {
+            w[16] |= l4 << 16;
+            w[17] = (l4 & 0xffffu) | (l4rem << 16);
+        }
+        if (status != RPKT_S_OK) {
+            w[0] |= status;
+            L.status = status;
+            return;
+        }
+    } else {
+        // round 2: Ipv4::parse (ipv4/generated.rs:35-51) and getters (:61-112, 269-288)
+        Hdr6 ip;
+        read_hdr(slot, ph + l3, ip);
+        const uint32_t vhl = ip.F[0] & 0xffu;
+        const uint32_t ihl4 = (vhl & 0xfu) * 4u;
+        const uint32_t tot = be16_hi(ip.F[0]);
+        if (rem < 20) status = RPKT_S_IP_SHORT;
+        else if (ihl4 < 20) status = RPKT_S_IP_BAD_IHL;
+        else if (ihl4 > rem) status = RPKT_S_IP_IHL_GT_LEN;
+        else if (tot < ihl4) status = RPKT_S_IP_TOT_LT_IHL;
+        else if (tot > rem) status = RPKT_S_IP_TOT_GT_LEN;
+        if (status != RPKT_S_OK) {
+            w[0] |= status;
+            L.status = status;
+            return;
+        }
+        proto = (ip.F[2] >> 8) & 0xffu;
+        const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
+        w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
+        w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
+        w[8] = (ip.F[2] & 0xffffu) | (be16_hi(ip.F[2]) << 16);
+        w[9] = src;
+        w[10] = dst;
+        if (flags & RPKT_F_IP_SUM)
+            w[18] = be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4), fr.off + l3);
+        l4 = l3 + ihl4;                                        // Ipv4::payload :115-127
+        l4rem = tot - ihl4;
+        w[16] |= l4 << 16;
+        w[17] = l4 | (l4rem << 16);
+        // pseudo header (smoltcp pseudo_header_v4): src, dst
+        paddr = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu);
     }
-    const uint32_t proto = (ip.F[2] >> 8) & 0xffu;
-    const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
-    w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
-    w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
-    w[8] = (ip.F[2] & 0xffffu) | (be16_hi(ip.F[2]) << 16);
-    w[9] = src;
-    w[10] = dst;
-    if (flags & RPKT_F_IP_SUM)
-        w[18] = be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4), fr.off + l3);
-    const uint32_t l4 = l3 + ihl4;                             // Ipv4::payload :115-127
-    const uint32_t l4rem = tot - ihl4;
-    w[16] |= l4 << 16;
-    w[17] = l4 | (l4rem << 16);
 
-    // round 3: Udp::parse (udp/generated.rs:31-42) / Tcp::parse (tcp/generated.rs:34-45)
+    // round 3: Udp::parse (udp/generated.rs:31-42) / Tcp::parse (tcp/generated.rs:34-45).
+    // An IPv4 L4 header always lies in the window (l4 <= 82); an IPv6 one past its
+    // extension headers may not: its fields are then read from global memory, and the
+    // in-window part of its sum is whatever of it the window holds.
     Hdr6 h4;
-    read_hdr(slot, ph + l4, h4);
+    read_hdr(slot, v6 && ph + l4 > (uint32_t)kWin ? (uint32_t)kWin : ph + l4, h4);
+    if (v6 && __builtin_expect(ph + l4 + 20u > (uint32_t)kWin, 0)) gread20(rs, fr.off + l4, h4.F);
     uint32_t l4len = 0;
     if (proto == 17u) {
         const uint32_t ulen = be16_lo(h4.F[1]);
@@ -769,7 +903,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
             w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
             w[14] = ulen;
             w[15] = be16_hi(h4.F[1]);
-            w[17] = (l4 + 8) | ((ulen - 8) << 16);             // Udp::payload :66-76
+            w[17] = ((l4 + 8) & 0xffffu) | ((ulen - 8) << 16);   // Udp::payload :66-76
             l4len = ulen;
         }
     } else if (proto == 6u) {
@@ -782,7 +916,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
             w[13] = bswap32(h4.F[2]);
             w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
             w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
-            w[17] = (l4 + hl) | ((l4rem - hl) << 16);          // Tcp::payload :125-131
+            w[17] = ((l4 + hl) & 0xffffu) | ((l4rem - hl) << 16);   // Tcp::payload :125-131
             l4len = l4rem;
         }
     } else {
@@ -792,15 +926,16 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     L.status = status;
     if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
         L.want_l4 = true;
-        // pseudo header (smoltcp pseudo_header_v4): src, dst, proto, length
-        L.pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto + l4len;
+        // pseudo header: addresses, protocol, length (smoltcp pseudo_header_v4 / _v6; the
+        // v6 u32 length is < 2^16 here, so one word)
+        L.pseudo = paddr + proto + l4len;
         const uint32_t win_end = kWin - ph;                    // frame offset where LDS ends
         const uint32_t e = l4 + l4len;
         const uint32_t e_in = e < win_end ? e : win_end;
         L.l4_part = raw_range_sum(slot, h4.R, h4.a0, ph + l4, ph + e_in);
         L.l4_start_abs = fr.off + l4;
         if (e > win_end) {
-            L.stream_s = fr.off + win_end;
+            L.stream_s = fr.off + (l4 > win_end ? l4 : win_end);
             L.stream_e = fr.off + e;
         }
     }
@@ -813,13 +948,15 @@ __device__ __forceinline__ uint64_t flow_event(const LaneRec& L, const uint32_t*
     uint64_t ev = w[19];
     uint32_t bucket = n_buckets;
     const uint32_t proto = (w[8] >> 8) & 0xffu;
-    const bool ip_parsed = L.status == RPKT_S_OK || L.status >= RPKT_S_L4_OTHER;
+    const bool ip4_parsed = !L.is6 && (L.status == RPKT_S_OK ||
+                                       (L.status >= RPKT_S_L4_OTHER && L.status <= RPKT_S_TCP_BAD_DOFF));
+    // words 9 / 10: the IPv4 addresses, or the IPv6 address folds
     if (L.status == RPKT_S_OK)
         bucket = flow_hash(w[9], w[10], w[11] & 0xffffu, w[11] >> 16, proto) % n_buckets;
     ev |= (uint64_t)bucket << 32;
-    if (ip_parsed && (w[18] & 0xffffu) != 0xffffu) ev |= 1ull << 48;
+    if (ip4_parsed && (w[18] & 0xffffu) != 0xffffu) ev |= 1ull << 48;
     if (L.status == RPKT_S_OK && (w[18] >> 16) != 0xffffu &&
-        !(proto == 17u && (w[15] & 0xffffu) == 0))
+        !(!L.is6 && proto == 17u && (w[15] & 0xffffu) == 0))
         ev |= 1ull << 49;
     return ev;
 }
@@ -830,10 +967,14 @@ __device__ __forceinline__ u32x4 compact_record(const LaneRec& L, uint32_t flags
     const uint32_t* w = L.w;
     const uint32_t proto = (w[8] >> 8) & 0xffu;
     uint32_t verdict = 0;
-    if ((flags & RPKT_F_IP_SUM) && (w[18] & 0xffffu) == 0xffffu) verdict |= 1u;
+    // IPv6: no header checksum; bit 0 = the IPv6 header parsed
+    const bool ip_ok = L.is6 ? (L.status != RPKT_S_IP6_SHORT && L.status != RPKT_S_IP6_BAD_LEN)
+                             : (w[18] & 0xffffu) == 0xffffu;
+    if ((flags & RPKT_F_IP_SUM) && ip_ok) verdict |= 1u;
     if ((flags & RPKT_F_L4_SUM) && L.status == RPKT_S_OK &&
-        ((w[18] >> 16) == 0xffffu || (proto == 17u && (w[15] & 0xffffu) == 0)))
+        ((w[18] >> 16) == 0xffffu || (!L.is6 && proto == 17u && (w[15] & 0xffffu) == 0)))
         verdict |= 2u;
+    if (L.is6) verdict |= 4u;
     return u32x4{(w[0] & 0xffffu) | (proto << 16) | (verdict << 24), w[16], w[17], w[18]};
 }
 

@@ -17,6 +17,8 @@
 #include <thread>
 #include <vector>
 
+#define RPKT_GEN_MAX_EXT 10
+
 namespace {
 
 struct Rng {
@@ -74,6 +76,16 @@ struct Spec {
     bool rand_payload = false;
     uint8_t payload_byte = 0xae;  // loopback_tx.rs:45
     int fault = 0;           // 0 none; 1 truncate; 2 bad ihl; 3 tot>len; 4 bad udp len/doff; 5 tot<ihl; 6 not ipv4; 7 other proto; 8 short L4
+    // IPv6 (configs 10-12): extension header chain (next-header values 0 HopByHop,
+    // 60 DestOptions, 43 Routing, 44 Fragment, 51 AH), the upper-layer protocol when it is
+    // neither TCP nor UDP (0 = by `tcp`), and IPv6 faults: 1 payload_len > remaining,
+    // 2 an extension header_len past the payload, 3 a non-atomic fragment, 4 AH header_len
+    // 8, 5 a payload_len that cuts the first extension header short
+    bool v6 = false;
+    int n_ext = 0;
+    uint8_t ext[RPKT_GEN_MAX_EXT] = {};
+    uint32_t v6_proto = 0;
+    int v6_fault = 0;
 };
 
 // Option bytes for an IPv4 header of `bytes` option space (NOP / RecordRoute / EOL).
@@ -199,8 +211,195 @@ void build(const Spec& s, uint32_t len, uint8_t* out, Rng& r) {
     memcpy(out, f, len);
 }
 
+// IPv6 options (Pad1 / PadN / RouterAlert / a generic type) filling `bytes` of a
+// HopByHop or DestOptions header (ipv6/generated.rs:1540-1552 types).
+void ipv6_options(uint8_t* o, int bytes, Rng& r) {
+    int i = 0;
+    while (i < bytes) {
+        int left = bytes - i;
+        uint32_t pick = r.below(4);
+        if (pick == 1 && left >= 4) { o[i] = 5; o[i + 1] = 2; put16(o + i + 2, r.below(3)); i += 4; }
+        else if (pick == 2 && left >= 3) {
+            int dl = std::min(left - 2, 1 + (int)r.below(6));
+            o[i] = (uint8_t)(r.below(2) ? 11 : 0xc2); o[i + 1] = (uint8_t)dl;
+            for (int k = 0; k < dl; k++) o[i + 2 + k] = (uint8_t)r.next();
+            i += 2 + dl;
+        } else if (left >= 2 && pick != 3) {
+            o[i] = 1; o[i + 1] = (uint8_t)(left - 2);             // PadN to the end
+            for (int k = 2; k < left; k++) o[i + k] = 0;
+            i = bytes;
+        } else { o[i++] = 0; }                                    // Pad1
+    }
+}
+
+// Byte length of extension header kind `t` in s (drawn once per frame by the caller).
+struct Ext6 { uint8_t type; uint32_t len; uint32_t rt_type, rt_n, rt_left; };
+
+// One IPv6 frame of exactly `len` bytes: Ether [+ tags] + IPv6 + the extension chain of
+// s.ext + UDP/TCP (or s.v6_proto), checksums with the IPv6 pseudo header over the
+// routing header's final address when segments are left (RFC 8200 section 8.1; the
+// product's own arithmetic, independent of oracle/).
+void build6(const Spec& s, uint32_t len, uint8_t* out, Rng& r) {
+    static thread_local uint8_t scratch[(1u << 16) + 2048];
+    const uint32_t cap = std::min<uint32_t>(std::max<uint32_t>(len, 512) + 512, sizeof(scratch));
+    memset(scratch, 0, cap);
+    uint8_t* f = scratch;
+    memcpy(f, kDmac, 6);
+    memcpy(f + 6, kSmac, 6);
+    uint32_t off = 12;
+    if (s.nvlan >= 1) {
+        put16(f + off, s.tpid0); off += 2;
+        put16(f + off, (r.below(8) << 13) | (r.below(2) << 12) | r.below(4096)); off += 2;
+    }
+    if (s.nvlan >= 2) {
+        put16(f + off, 0x8100); off += 2;
+        put16(f + off, (r.below(8) << 13) | (r.below(2) << 12) | r.below(4096)); off += 2;
+    }
+    put16(f + off, 0x86dd); off += 2;
+    const uint32_t l3 = off;
+    // extension header sizes
+    Ext6 e[RPKT_GEN_MAX_EXT];
+    uint32_t ext_total = 0;
+    for (int k = 0; k < s.n_ext; k++) {
+        Ext6& x = e[k];
+        x.type = s.ext[k];
+        x.rt_type = x.rt_n = x.rt_left = 0;
+        switch (x.type) {
+            case 0: case 60: x.len = 8 * (1 + r.below(3)); break;
+            case 43: {
+                uint32_t pick = r.below(3);
+                x.rt_type = pick == 0 ? 0 : (pick == 1 ? 4 : 2);
+                x.rt_n = x.rt_type == 2 ? 1 : 1 + r.below(3);
+                x.rt_left = r.below(x.rt_n + 1);
+                x.len = 8 + 16 * x.rt_n;
+                break;
+            }
+            case 44: x.len = 8; break;
+            default: x.len = 12 + 4 * r.below(4); break;           // 51 AH
+        }
+        ext_total += x.len;
+    }
+    const uint32_t up = s.v6_proto ? s.v6_proto : (s.tcp ? 6u : 17u);
+    const uint32_t l4h = up == 6 ? (uint32_t)s.doff * 4 : (up == 17 ? 8u : 8u);
+    int64_t plen = (int64_t)len - l3 - 40 - s.pad;
+    if (plen < (int64_t)(ext_total + l4h)) plen = ext_total + l4h;
+    if (plen > 65535) plen = 65535;
+    const uint32_t l4 = l3 + 40 + ext_total;
+    const uint32_t l4len = (uint32_t)plen - ext_total;
+    // payload
+    uint8_t* pl = f + l4 + l4h;
+    for (int64_t k = 0; k < (int64_t)l4len - l4h; k++)
+        pl[k] = s.rand_payload ? (uint8_t)r.next() : s.payload_byte;
+    // IPv6 header (ipv6/generated.rs:16-20 template, setters :107-135)
+    uint8_t* ip = f + l3;
+    put32(ip, (6u << 28) | (r.below(256) << 20) | r.below(1u << 20));
+    put16(ip + 4, (uint32_t)plen);
+    ip[6] = (uint8_t)(s.n_ext ? s.ext[0] : up);
+    ip[7] = (uint8_t)(1 + r.below(255));
+    put32(ip + 8, 0x20010db8u); put32(ip + 12, 0); put32(ip + 16, (uint32_t)r.next());
+    put32(ip + 20, s.src);
+    put32(ip + 24, 0x20010db8u); put32(ip + 28, 0xffff0000u); put32(ip + 32, 0);
+    put32(ip + 36, s.dst);
+    const uint8_t* pdst = ip + 24;
+    // extension headers
+    uint32_t c = l3 + 40;
+    for (int k = 0; k < s.n_ext; k++) {
+        uint8_t* h = f + c;
+        const Ext6& x = e[k];
+        h[0] = (uint8_t)(k + 1 < s.n_ext ? s.ext[k + 1] : up);
+        switch (x.type) {
+            case 0: case 60:
+                h[1] = (uint8_t)(x.len / 8 - 1);
+                ipv6_options(h + 2, (int)x.len - 2, r);
+                break;
+            case 43:
+                h[1] = (uint8_t)(x.len / 8 - 1);
+                h[2] = (uint8_t)x.rt_type;
+                h[3] = (uint8_t)x.rt_left;
+                put32(h + 4, x.rt_type == 4 ? ((x.rt_n - 1) << 24) : 0);
+                for (uint32_t a = 0; a < x.rt_n; a++) {
+                    put32(h + 8 + 16 * a, 0x20010db8u); put32(h + 12 + 16 * a, 0xeeee0000u + a);
+                    put32(h + 16 + 16 * a, (uint32_t)r.next()); put32(h + 20 + 16 * a, (uint32_t)r.next());
+                }
+                if (x.rt_left > 0)
+                    pdst = h + 8 + (x.rt_type == 4 ? 0 : 16 * (x.rt_n - 1));
+                break;
+            case 44:
+                h[1] = 0;
+                put16(h + 2, s.v6_fault == 3 ? ((1 + r.below(8000)) << 3) | r.below(2) : 0);
+                put32(h + 4, (uint32_t)r.next());
+                break;
+            default:
+                h[1] = (uint8_t)(x.len / 4 - 2);
+                put32(h + 4, (uint32_t)r.next());
+                put32(h + 8, (uint32_t)r.next());
+                for (uint32_t k2 = 12; k2 < x.len; k2++) h[k2] = (uint8_t)r.next();
+                break;
+        }
+        c += x.len;
+    }
+    // L4 header and its checksum over the IPv6 pseudo header (src, final dst, u32 length,
+    // next header)
+    uint8_t* h4 = f + l4;
+    put16(h4, s.sport);
+    put16(h4 + 2, s.dport);
+    if (up == 6) {
+        put32(h4 + 4, (uint32_t)r.next());
+        put32(h4 + 8, (uint32_t)r.next());
+        put16(h4 + 12, ((uint32_t)s.doff << 12) | 0x10 | (r.below(2) << 3));
+        put16(h4 + 14, 1024 + r.below(60000));
+        put16(h4 + 16, 0);
+        put16(h4 + 18, 0);
+        tcp_options(h4 + 20, (int)l4h - 20, r);
+    } else if (up == 17) {
+        put16(h4 + 4, l4len);
+        put16(h4 + 6, 0);
+    } else {
+        for (uint32_t k = 4; k < 8; k++) h4[k] = (uint8_t)r.next();
+    }
+    if (up == 6 || up == 17) {
+        uint32_t ps = ones_sum(ip + 8, 16, 0);
+        ps = ones_sum(pdst, 16, ps);
+        ps += (l4len >> 16) + (l4len & 0xffff) + up;
+        uint32_t ck = (~ones_sum(h4, l4len, ps)) & 0xffff;
+        if (up == 17 && ck == 0) ck = 0xffff;                    // RFC 768 / 8200
+        if (s.bad_l4) { ck ^= 0x5a5a; if (ck == 0) ck = 1; }
+        if (up == 17 && s.udp_zero) ck = 0;
+        put16(h4 + (up == 6 ? 16 : 6), ck);
+    }
+    // structural faults (after the checksums)
+    switch (s.v6_fault) {
+        case 1: put16(ip + 4, (uint32_t)plen + 1 + r.below(64)); break;   // payload_len > remaining
+        case 2:
+            if (s.n_ext) f[l3 + 40 + 1] = (uint8_t)(200 + r.below(56));    // header_len past the payload
+            break;
+        case 5:                                                           // first extension header cut short
+            if (s.n_ext) put16(ip + 4, r.below(2));
+            break;
+        case 4: {                                                         // AH with header_len 8
+            uint32_t cc = l3 + 40;
+            for (int k = 0; k < s.n_ext; k++) {
+                if (e[k].type == 51) { f[cc + 1] = 0; break; }
+                cc += e[k].len;
+            }
+            break;
+        }
+        default: break;
+    }
+    switch (s.fault) {
+        case 4:
+            if (up == 6) h4[12] = (uint8_t)((r.below(5)) << 4);
+            else if (up == 17) put16(h4 + 4, r.chance(5000) ? r.below(8) : l4len + 1 + r.below(16));
+            break;
+        case 8: put16(ip + 4, ext_total + r.below(up == 6 ? 20 : 8)); break;   // L4 too short
+        default: break;
+    }
+    memcpy(out, f, len);
+}
+
 // config: 1 bench_rpkt (1k x 64B UDP, rpkt_build.rs header values), 2 64B UDP,
-// 3 1500B TCP, 4 IMIX mixed, 5 VLAN/QinQ + options TCP, 6 fuzz (all statuses).
+// 3 1500B TCP, 4 IMIX mixed, 5 VLAN/QinQ + options TCP, 6 fuzz (all statuses),
+// 10 / 11 dual stack 64 B / 1500 B, 12 dual-stack fuzz (every IPv4 and IPv6 status).
 Spec spec_for(int config, uint64_t seed, uint32_t i, uint32_t len, Rng& r) {
     Spec s;
     switch (config) {
@@ -237,6 +436,54 @@ Spec spec_for(int config, uint64_t seed, uint32_t i, uint32_t len, Rng& r) {
             s.pad = r.chance(1000) ? (int)r.below(9) : 0;
             s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
             break;
+        case 10:  // dual stack, 64 B: IPv4/UDP (config 2's flows) or IPv6/UDP, 50/50
+            s.v6 = r.below(2) == 1;
+            s.src = gen_ip(172, 74, 8192, i);
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            s.ttl = 64; s.ident = i & 0xffff;
+            break;
+        case 11: {  // dual stack, 1500 B: IPv4 or IPv6 (0-3 extension headers), TCP or UDP
+            static const uint8_t kExt[5] = {0, 60, 43, 44, 51};
+            s.v6 = r.below(2) == 1;
+            s.nvlan = r.below(4) == 0 ? 1 : 0;
+            s.tcp = r.below(2) == 1; s.src = gen_ip(172, 74, 8192, r.below(8192));
+            s.sport = 1024 + r.below(60000); s.dport = s.tcp ? 443 : 4433;
+            s.rand_payload = true;
+            s.bad_ip = r.chance(100); s.bad_l4 = r.chance(100);
+            s.ident = i & 0xffff;
+            if (s.v6) {
+                s.n_ext = (int)r.below(4);
+                for (int k = 0; k < s.n_ext; k++) s.ext[k] = kExt[r.below(5)];
+            }
+            break;
+        }
+        case 12: {  // dual-stack fuzz: every IPv4 and IPv6 status (configs 6's IPv4 faults)
+            static const uint8_t kExt[5] = {0, 60, 43, 44, 51};
+            static const uint8_t kOther[6] = {58, 50, 59, 89, 47, 1};
+            s.v6 = r.below(3) != 0;
+            s.nvlan = (int)r.below(4) == 0 ? (int)r.below(3) : 0;
+            s.tpid0 = r.below(2) ? 0x88a8 : 0x8100;
+            s.ihl = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            s.tcp = r.below(2) == 1;
+            s.doff = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            s.src = (uint32_t)r.next(); s.dst = (uint32_t)r.next();
+            s.sport = r.below(65536); s.dport = r.below(65536);
+            s.rand_payload = true;
+            s.pad = r.below(8) == 0 ? (int)r.below(12) : 0;
+            s.bad_ip = r.chance(1000); s.bad_l4 = r.chance(1000);
+            s.udp_zero = r.chance(500);
+            if (s.v6) {
+                s.n_ext = r.below(16) == 0 ? 7 + (int)r.below(3) : (int)r.below(4);
+                for (int k = 0; k < s.n_ext; k++) s.ext[k] = kExt[r.below(5)];
+                if (r.below(8) == 0) s.v6_proto = kOther[r.below(6)];
+                const uint32_t f6 = r.below(12);
+                s.v6_fault = f6 < 5 ? (int)f6 + 1 : 0;
+                s.fault = r.below(6) == 0 ? (r.below(3) == 0 ? 4 : (r.below(2) ? 8 : 1)) : 0;
+            } else {
+                s.fault = r.below(4) == 0 ? 1 + (int)r.below(8) : 0;
+            }
+            break;
+        }
         case 7:  // jumbo frames (rpkt-dpdk/examples/jumboframe_tx.rs:45, PACKET_LEN 8000)
             s.tcp = r.below(2) == 1; s.src = gen_ip(172, 74, 8192, r.below(8192));
             s.sport = 1024 + r.below(4096); s.dport = s.tcp ? 80 : 161;
@@ -272,14 +519,17 @@ void fill_range(int config, uint64_t seed, uint64_t first, const uint32_t* offse
         uint32_t len = lens[i];
         uint64_t off = offsets ? offsets[i] : (uint64_t)i * stride;
         Spec s = spec_for(config, seed, (uint32_t)gi, len, r);
-        if ((config == 6 || config == 8) && s.fault == 1) {
+        if ((config == 6 || config == 8 || config == 12) && s.fault == 1) {
             // truncation: build a full frame then cut it at a random length
             uint32_t full = len + 64;
             std::vector<uint8_t> tmp(full);
             Spec s2 = s;
             s2.fault = 0;
-            build(s2, full, tmp.data(), r);
+            if (s2.v6) build6(s2, full, tmp.data(), r);
+            else build(s2, full, tmp.data(), r);
             memcpy(frames + off, tmp.data(), len);
+        } else if (s.v6) {
+            build6(s, len, frames + off, r);
         } else {
             build(s, len, frames + off, r);
         }
@@ -297,8 +547,8 @@ void rpkt_gen_lengths(int config, uint64_t seed, uint64_t first, uint32_t n, uin
         Rng r(seed * 0x2545f4914f6cdd1dull ^ (0xd1b54a32d192ed03ull * (first + i + 1)));
         uint32_t L;
         switch (config) {
-            case 1: case 2: L = 64; break;
-            case 3: L = 1500; break;
+            case 1: case 2: case 10: L = 64; break;
+            case 3: case 11: L = 1500; break;
             case 4: { uint32_t k = r.below(12); L = k < 7 ? 64 : (k < 11 ? 570 : 1500); break; }
             case 5: L = 64 + r.below(1518 - 64 + 1); break;
             case 7: L = 8000; break;

@@ -140,10 +140,12 @@ struct OptSlices {
     bool need;
 };
 
+// is6: an IPv6 record (RPKT_F_IPV6): no IPv4 option slice; its TCP slice as any other
 __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto, uint32_t l3,
-                                                uint32_t l4, uint32_t doff4) {
+                                                uint32_t l4, uint32_t doff4, bool is6) {
     OptSlices S;
-    S.ip_parsed = status == RPKT_S_OK || status >= RPKT_S_L4_OTHER;
+    S.ip_parsed = !is6 && (status == RPKT_S_OK ||
+                           (status >= RPKT_S_L4_OTHER && status <= RPKT_S_TCP_BAD_DOFF));
     S.tcp = status == RPKT_S_OK && proto == 6u;
     S.ip_lo = l3 + 20u;
     S.ip_hi = S.ip_parsed ? l4 : S.ip_lo;

@@ -24,7 +24,7 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
     const uint32_t* w = L.w;
     const uint32_t l3 = w[16] & 0xffffu, l4 = w[16] >> 16;
     const OptSlices S = opt_slices(L.status, (w[8] >> 8) & 0xffu, l3, l4,
-                                   ((w[14] >> 12) & 0xfu) * 4u);
+                                   ((w[14] >> 12) & 0xfu) * 4u, L.is6);
     const uint32_t ph = fr.off & 15u;
     // every byte the walks use lies below need_hi (OptWin::dw's dword pair may read up to
     // 7 B past it: window padding or the next slot, never used)
@@ -140,7 +140,7 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
         for (int k = 0; k < 20; ++k) L.w[k] = x + k;
         L.status = 0;
     } else {
-        parse_lane(W, lane, fr, valid, flags, L);
+        parse_lane(W, lane, fr, valid, flags, L, rs);
     }
     if constexpr (OPTS) options_from_window(W, rs, frames_bytes, lane, fr, L, opt_rules, opts, p0, n);
     if constexpr (V != 3 && !C16) stage_record(W, lane, L.w);
@@ -275,13 +275,6 @@ struct ChainSrc {
     }
 };
 
-// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout)
-__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t (&F)[5]) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k)
-        F[k] = gbyte(rs, a + 4 * k) | (gbyte(rs, a + 4 * k + 1) << 8) |
-               (gbyte(rs, a + 4 * k + 2) << 16) | (gbyte(rs, a + 4 * k + 3) << 24);
-}
 // checksum::from_slice over n bytes at absolute `a` (rpkt/src/checksum.rs:33-62)
 __device__ __forceinline__ uint32_t gsum_be(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t n) {
     uint32_t acc = 0, k = 0;
@@ -323,6 +316,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
     const uint32_t C = s0.len;                                 // Pbuf::new, pbuf.rs:19-34
     L.stream_s = L.stream_e = L.l4_part = L.l4_start_abs = L.pseudo = 0;
     L.want_l4 = false;
+    L.is6 = false;
     w[19] = pkt;
     uint32_t status = RPKT_S_OK;
 
@@ -975,11 +969,14 @@ __global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
     out[p] = (uint16_t)fold16(acc);
 }
 
+// flags the batch / ring / fused-option parses accept
+constexpr uint32_t kParseFlags = RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV | RPKT_F_IPV6;
+
 // shared checks of the parse entry points
 int parse_args_ok(const rpkt_batch_t* b, uint32_t flags, const void* recs_dev,
                          const void* flow_ev_dev, uint32_t n_buckets) {
     if (!b || !recs_dev) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (flags & ~kParseFlags) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
@@ -1014,13 +1011,13 @@ template <bool C16>
 int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
                       uint32_t n_buckets, void* stream) {
     if (n_slots && !slots) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (flags & ~kParseFlags) return RPKT_E_INVAL;
     const bool fev = (flags & RPKT_F_FLOW_EV) != 0;
-    if (fev && (n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)) return RPKT_E_INVAL;
     for (uint32_t k = 0; k < n_slots; ++k) {                      // all checked, then launched
         const rpkt_ring_slot_t& q = slots[k];
         const rpkt_batch_t& b = q.batch;
-        if (b.n == 0) continue;
+        if (b.n == 0) continue;                // as rpkt_gpu_parse_batch with n == 0: RPKT_OK
+        if (fev && (n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS)) return RPKT_E_INVAL;
         if (!b.frames_dev || !q.recs_dev) return RPKT_E_INVAL;
         if (b.frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
         if (!b.offsets_dev && b.stride == 0) return RPKT_E_INVAL;
@@ -1122,7 +1119,7 @@ uint32_t rpkt_flow_hash(uint32_t ip_src, uint32_t ip_dst, uint16_t sp, uint16_t 
 int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs_dev,
                          rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!b || !recs_dev) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (flags & ~kParseFlags) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
@@ -1163,7 +1160,7 @@ int rpkt_gpu_parse_ring_compact(const rpkt_ring_slot_t* slots, uint32_t n_slots,
 int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev,
                                  rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!b || !recs_dev) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (flags & ~kParseFlags) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
@@ -1202,6 +1199,7 @@ int rpkt_gpu_parse_options_batch_compact(const rpkt_batch_t* b, uint32_t flags,
 int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,
                           rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!c || !recs_dev) return RPKT_E_INVAL;
+    // the chain parse is IPv4-only (RPKT_F_IPV6 is not accepted)
     if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
     if (c->n_chains == 0) return RPKT_OK;
     if (!c->chain_first_dev || (c->n_segs && (!c->buf_dev || !c->segs_dev))) return RPKT_E_INVAL;
@@ -1310,13 +1308,20 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
 static int flow_hist_attr_once() {
     static std::mutex mu;
     static uint64_t done[4] = {0, 0, 0, 0};          // bit d: device d (up to 256 devices)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 256) dev = 0;
+    int dev = -1;
+    {
+        const int rc = hip_check(hipGetDevice(&dev));
+        if (rc) return rc;
+    }
+    auto set = [] {
+        return hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+    };
+    if (dev < 0 || dev >= 256) return set();         // not cached: set on every call
     std::lock_guard<std::mutex> g(mu);
     if (done[dev >> 6] & (1ull << (dev & 63))) return RPKT_OK;
-    const int rc = hip_check(hipFuncSetAttribute((const void*)flow_hist_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 3 * (kFlowLdsMax + 1) * sizeof(uint32_t)));
+    const int rc = set();
     if (rc == RPKT_OK) done[dev >> 6] |= 1ull << (dev & 63);
     return rc;
 }

@@ -273,7 +273,13 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     const uint32_t doff4 = ((w[14] >> 12) & 0xfu) * 4u;
     const uint32_t l4hdr = proto == 17u ? 8u : (proto == 6u ? doff4 : 0u);
     const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
-    const bool ok = valid && nv <= RPKT_MAX_VLAN && ihl4 >= 20u && !(proto == 6u && doff4 < 20u) &&
+    // the build writes IPv4 headers: an IPv6 record (RPKT_F_IPV6 parse: dispatched on
+    // 0x86DD) is not built
+    const uint32_t st = w[0] & 0xffu;
+    const uint32_t det = nv == 0u ? w[0] >> 16 : (nv == 1u ? w[5] & 0xffffu : w[5] >> 16);
+    const bool rec6 = det == 0x86ddu && st != RPKT_S_ETH_SHORT && st != RPKT_S_VLAN_SHORT &&
+                      st != RPKT_S_NOT_IPV4;
+    const bool ok = valid && !rec6 && nv <= RPKT_MAX_VLAN && ihl4 >= 20u && !(proto == 6u && doff4 < 20u) &&
                     len >= l4 + l4hdr && len - l3 <= 65535u &&
                     !(proto == 17u && len - l4 > 65535u);
     const bool fill_ip = ok && (flags & RPKT_BUILD_IP_CSUM);
@@ -385,7 +391,7 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         return;
     }
     LaneRec L;
-    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L);
+    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L, rs);
     uint8_t* slot = &W.win[lane * kSlot];
     uint8_t* s = slot + (fr.off & 15u);
     {

@@ -50,6 +50,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 
     // records of the tile (coalesced): status, IP protocol, l3 / l4 offsets, TCP doff
     uint32_t status, proto, l3, l4, doff4;
+    bool is6;                                            // an IPv6 record (RPKT_F_IPV6)
     if constexpr (C16) {
         const u32x4* in = reinterpret_cast<const u32x4*>(recs_any);
         const u32x4 r = i < n ? __builtin_nontemporal_load(&in[i]) : u32x4{0u, 0u, 0u, 0u};
@@ -58,6 +59,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         l3 = r.y & 0xffffu;
         l4 = r.y >> 16;
         doff4 = (r.z & 0xffffu) - l4;                    // payload_off - l4: TCP, status OK
+        is6 = ((r.x >> 24) & 4u) != 0u;                  // verdict bit 2
     } else {
         const rpkt_rec_t* recs = reinterpret_cast<const rpkt_rec_t*>(recs_any);
         const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
@@ -82,14 +84,20 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         wave_sync();
         const uint32_t w0 = st[lane * 21 + 0], w8 = st[lane * 21 + 8];
         const uint32_t w14 = st[lane * 21 + 14], w16 = st[lane * 21 + 16];
+        const uint32_t w5 = st[lane * 21 + 5];
         wave_sync();
         status = w0 & 0xffu;
+        // the dispatch ethertype: the outer one, or the last VLAN tag's
+        const uint32_t nv = (w0 >> 8) & 0xffu;
+        const uint32_t et = nv == 0u ? w0 >> 16 : (nv == 1u ? w5 & 0xffffu : w5 >> 16);
+        is6 = et == 0x86ddu && status != RPKT_S_ETH_SHORT && status != RPKT_S_VLAN_SHORT &&
+              status != RPKT_S_NOT_IPV4;
         proto = (w8 >> 8) & 0xffu;
         l3 = w16 & 0xffffu;
         l4 = w16 >> 16;
         doff4 = ((w14 >> 12) & 0xfu) * 4u;
     }
-    const OptSlices S = opt_slices(status, proto, l3, l4, doff4);
+    const OptSlices S = opt_slices(status, proto, l3, l4, doff4, is6);
     const uint32_t need_lo = S.need_lo, need_hi = S.need_hi;
     const bool need = S.need;
 

@@ -61,6 +61,13 @@ def reduce_counters(counters, group=None, *, n_buckets=None, stream=None, via="a
     all-reduce.  A gloo group (CPU rehearsals) always sums through torch.distributed.
     The path taken is in dist.last_reduce_path."""
     global last_reduce_path, last_reduce_error
+    if isinstance(group, int) and not isinstance(group, bool):
+        # the round-2 signature reduce_counters(counters, n_buckets): still accepted
+        import warnings
+        warnings.warn("reduce_counters(counters, n_buckets) is deprecated: pass "
+                      "n_buckets=... (the second positional argument is the process group)",
+                      DeprecationWarning, stacklevel=2)
+        group, n_buckets = None, group
     last_reduce_error = None
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         last_reduce_path = "local"

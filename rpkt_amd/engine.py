@@ -259,16 +259,33 @@ def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, st
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
 
 
-def ring_slots(batches, recs, flow_evs=None):
+def ring_slots(batches, recs, flow_evs=None, compact=None):
     """The rpkt_ring_slot_t array of a receive ring: batch k, its record tensor and
     (optional) its flow-event tensor.  Build it once per ring and pass it to parse_ring
     on every pass: it holds device addresses only, so the batches and tensors must stay
-    alive (and in place) as long as the array is used."""
+    alive (and in place) as long as the array is used.  Every batch needs its record
+    tensor (and flow-event tensor), each large enough for its frames: 80-B records, or
+    16-B ones with compact=True (compact=None: either, checked again by parse_ring)."""
+    if len(recs) != len(batches) or (flow_evs is not None and len(flow_evs) != len(batches)):
+        raise RpktError("ring_slots: %d batches, %d record tensors, %s flow-event tensors"
+                        % (len(batches), len(recs), len(flow_evs) if flow_evs is not None
+                           else "no"))
     arr = (RingSlot * len(batches))()
+    small = []
     for k, (db, r) in enumerate(zip(batches, recs)):
+        have = r.numel() * r.element_size()
+        if have < db.n * (REC16_BYTES if compact else REC_BYTES):
+            if compact is False or have < db.n * REC16_BYTES:
+                raise RpktError("ring_slots: slot %d holds %d record bytes for %d frames"
+                                % (k, have, db.n))
+            small.append(k)
+        if flow_evs is not None and flow_evs[k].numel() * flow_evs[k].element_size() < 8 * db.n:
+            raise RpktError("ring_slots: slot %d flow-event tensor too small" % k)
         arr[k].batch = db.desc()
         arr[k].recs_dev = r.data_ptr()
         arr[k].flow_ev_dev = flow_evs[k].data_ptr() if flow_evs is not None else None
+    # record bytes the slots can hold: 80-B parses refused by parse_ring if any is 16-B sized
+    arr._rpkt_compact_only = bool(small)
     return arr
 
 
@@ -276,6 +293,8 @@ def parse_ring(slots, flags=3, n_buckets=0, stream=None, compact=False):
     """rpkt_gpu_parse_ring[_compact]: every slot of `slots` (ring_slots(), with 80-B or,
     compact, 16-B record tensors) parsed as by parse_batch[_compact],
     RPKT_RING_MAX_SLOTS slots per kernel launch."""
+    if not compact and getattr(slots, "_rpkt_compact_only", False):
+        raise RpktError("parse_ring: some slot's records are sized for 16-B compact records")
     fn = lib().rpkt_gpu_parse_ring_compact if compact else lib().rpkt_gpu_parse_ring
     rc = fn(slots, len(slots), flags, n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_ring%s" % ("_compact" if compact else ""))

@@ -14,6 +14,14 @@ Config ids follow BASELINE.json `configs` (1-based like SURVEY.md §8d):
     and header-boundary positions (empty segments included), odd slot alignments
   9 protocol mix for the layer walk: 1,048,576 frames drawn from the reference's
     captures, a third cut short and a third with random header bytes (make_mix)
+ 10 dual stack, 1,048,576 x 64 B, stride 64: IPv4/UDP or IPv6/UDP at 50/50, 1 % bad
+    L4 (and IPv4 header) checksums; parsed with RPKT_F_IPV6
+ 11 dual stack, 1,048,576 x 1500 B, stride 1500: IPv4 or IPv6 with 0-3 extension
+    headers (HopByHop, DestOptions, Routing types 0/2/4 with segments left or not,
+    atomic Fragment, AH), TCP or UDP, a quarter 802.1Q-tagged, 1 % bad checksums
+ 12 dual-stack fuzz: every IPv4 and IPv6 status (truncation, bad payload_len, bad or
+    short extension headers, non-atomic fragments, chains past RPKT_MAX_IP6_EXT,
+    other upper-layer protocols, UDP checksum 0 over IPv6), packed
 """
 import ctypes
 import os
@@ -23,11 +31,13 @@ import numpy as np
 from .build import GEN_LIB, build_gen
 
 DEFAULT_N = {1: 1000, 2: 1 << 20, 3: 1 << 20, 4: 8 << 20, 5: 4 << 20, 6: 1 << 16,
-             7: 1 << 18, 8: 1 << 15, 9: 1 << 20}
-DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9}
-STRIDED = {1: 64, 2: 64, 3: 1500}
+             7: 1 << 18, 8: 1 << 15, 9: 1 << 20, 10: 1 << 20, 11: 1 << 20, 12: 1 << 16}
+DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9, 10: 10, 11: 11, 12: 12}
+STRIDED = {1: 64, 2: 64, 3: 1500, 10: 64, 11: 1500}
 CHAINED = (7, 8)
-FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3}   # config 2 = extract + IPv4 header sum
+DUAL_STACK = (10, 11, 12)                                 # generated with IPv6 frames
+# config 2 = extract + IPv4 header sum; the dual-stack configs parse with RPKT_F_IPV6
+FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3, 10: 11, 11: 11, 12: 11}
 MBUF_ROOM, MBUF_HEADROOM = 2048, 128                      # RTE_MBUF_DEFAULT_DATAROOM, headroom
 # header-boundary cut positions for the chain fuzz (Ether 14, tags 18/22, IPv4 +20..60, L4 +8/20)
 FUZZ_CUTS = (0, 1, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 26, 30, 33, 34, 35, 38,

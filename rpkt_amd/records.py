@@ -35,11 +35,34 @@ def project16(recs, flags):
     for k in ("status", "n_vlan", "ip_protocol", "l3_off", "l4_off", "payload_off",
               "payload_len", "ip_sum", "l4_sum"):
         out[k] = recs[k]
-    ip_ok = (recs["ip_sum"] == 0xffff) & bool(flags & 1)
-    l4_ok = bool(flags & 2) & (recs["status"] == 0) & (
-        (recs["l4_sum"] == 0xffff) | ((recs["ip_protocol"] == 17) & (recs["l4_checksum"] == 0)))
-    out["verdict"] = ip_ok.astype(np.uint8) | (l4_ok.astype(np.uint8) << 1)
+    v6 = is_ip6(recs)
+    ip6_parsed = v6 & ~np.isin(recs["status"], [STATUS["IP6_SHORT"], STATUS["IP6_BAD_LEN"]])
+    ip_ok = np.where(v6, ip6_parsed, recs["ip_sum"] == 0xffff) & bool(flags & F_IP_SUM)
+    l4_ok = bool(flags & F_L4_SUM) & (recs["status"] == 0) & (
+        (recs["l4_sum"] == 0xffff) |
+        (~v6 & (recs["ip_protocol"] == 17) & (recs["l4_checksum"] == 0)))
+    out["verdict"] = (ip_ok.astype(np.uint8) | (l4_ok.astype(np.uint8) << 1) |
+                      (v6.astype(np.uint8) << 2))
     return out
+
+
+def dispatch_ethertype(recs):
+    """The ethertype the IP parse was chosen on: ethertype, or the last VLAN tag's."""
+    nv = recs["n_vlan"].astype(np.int64)
+    last = recs["vlan_ethertype"][np.arange(recs.shape[0]), np.clip(nv - 1, 0, 1)]
+    return np.where(nv > 0, last, recs["ethertype"])
+
+
+def is_ip6(recs):
+    """Records that hold the IPv6 block (include/rpkt_gpu.h): dispatched to Ipv6::parse."""
+    pre = np.isin(recs["status"], [STATUS["ETH_SHORT"], STATUS["VLAN_SHORT"], STATUS["NOT_IPV4"]])
+    return ~pre & (dispatch_ethertype(recs) == 0x86DD)
+
+
+def ip6_block(recs):
+    """The IPv6 view of record bytes 24..43 (include/rpkt_gpu.h) as a structured array."""
+    raw = np.ascontiguousarray(recs).view(np.uint8).reshape(-1, REC_BYTES)[:, 24:44]
+    return np.ascontiguousarray(raw).view(IP6_BLOCK_DTYPE).reshape(-1)
 
 
 def as_records16(raw):
@@ -55,6 +78,8 @@ STATUS = {
     "OK": 0, "ETH_SHORT": 1, "VLAN_SHORT": 2, "NOT_IPV4": 3, "IP_SHORT": 4,
     "IP_BAD_IHL": 5, "IP_IHL_GT_LEN": 6, "IP_TOT_LT_IHL": 7, "IP_TOT_GT_LEN": 8,
     "L4_OTHER": 9, "UDP_SHORT": 10, "UDP_BAD_LEN": 11, "TCP_SHORT": 12, "TCP_BAD_DOFF": 13,
+    "IP6_SHORT": 14, "IP6_BAD_LEN": 15, "IP6_EXT_SHORT": 16, "IP6_EXT_BAD_LEN": 17,
+    "IP6_FRAGMENT": 18,
 }
 STATUS_NAME = {v: k for k, v in STATUS.items()}
 
@@ -62,8 +87,17 @@ STATUS_NAME = {v: k for k, v in STATUS.items()}
 F_IP_SUM = 1
 F_L4_SUM = 2
 F_FLOW_EV = 4
+F_IPV6 = 8
 
 MAX_VLAN = 2
+MAX_IP6_EXT = 8
+
+IP6_BLOCK_DTYPE = np.dtype([      # rpkt_rec_t bytes 24..43 of an IPv6 record
+    ("ip6_vtcfl", "<u4"), ("ip6_payload_len", "<u2"), ("ip6_next_header", "u1"),
+    ("ip6_hop_limit", "u1"), ("ip6_n_ext", "u1"), ("ip_protocol", "u1"), ("ip6_pdst_off", "<u2"),
+    ("ip6_src_fold", "<u4"), ("ip6_dst_fold", "<u4"),
+])
+assert IP6_BLOCK_DTYPE.itemsize == 20
 FLOW_MAX_BUCKETS = 65535
 
 

@@ -7,6 +7,8 @@ The reference exposes header views over a byte buffer (`T: Buf`) with
   Ipv4        rpkt/src/ipv4/generated.rs:17-127, 269-288
   Udp         rpkt/src/udp/generated.rs:13-76
   Tcp         rpkt/src/tcp/generated.rs:16-131
+  Ipv6 and its extension headers (RPKT_F_IPV6 records)
+              rpkt/src/ipv6/generated.rs:22-216, 224-999
 The engine already walked that chain on the GPU and left one rpkt_rec_t per
 frame; these classes re-expose it under the same names, argument meaning and
 Ok/Err behaviour, so code written against rpkt's chain reads the same:
@@ -21,7 +23,11 @@ returned Ok for this frame, and Err(buf) otherwise (buf = the unchanged
 cursor, as in ipv4/generated.rs:37,48).  Payload cursors carry (offset, len)
 within the frame; `chunk()` needs the frame bytes to have been supplied.
 """
-from .records import STATUS, MAX_VLAN
+import ipaddress
+
+import numpy as np
+
+from .records import STATUS, MAX_VLAN, ip6_block, is_ip6
 
 
 class EtherType:
@@ -40,12 +46,20 @@ class EtherType:
 
 class IpProtocol:
     """rpkt/src/ipv4/mod.rs:107-155 (subset on the path + common values)"""
+    IPV6_HOP_BY_HOP_OPTS = 0
     ICMP = 1
     IGMP = 2
     IPIP = 4
     TCP = 6
     UDP = 17
+    IPV6_ROUTE = 43
+    IPV6_FRAG = 44
     GRE = 47
+    ESP = 50
+    AH = 51
+    ICMPV6 = 58
+    IPV6_NO_NXT = 59
+    IPV6_DEST_OPTS = 60
 
 
 class Result:
@@ -121,6 +135,11 @@ def _st(rec):
 _IP_FAIL = {STATUS[k] for k in ("IP_SHORT", "IP_BAD_IHL", "IP_IHL_GT_LEN", "IP_TOT_LT_IHL",
                                  "IP_TOT_GT_LEN")}
 _PRE_IP = {STATUS["ETH_SHORT"], STATUS["VLAN_SHORT"], STATUS["NOT_IPV4"]} | _IP_FAIL
+_IP6_FAIL = {STATUS["IP6_SHORT"], STATUS["IP6_BAD_LEN"]}
+
+
+def _rec_is_ip6(rec):
+    return bool(is_ip6(np.asarray(rec).reshape(1))[0])
 
 
 class EtherFrame:
@@ -288,7 +307,7 @@ class Ipv4:
         """ipv4/generated.rs:35-51."""
         rec = buf.rec
         if (buf.stage != "l3" or buf.vlan_idx != int(rec["n_vlan"])
-                or _st(rec) in _PRE_IP):
+                or _st(rec) in _PRE_IP or _rec_is_ip6(rec)):
             return Err(buf)
         return Ok(Ipv4(buf))
 
@@ -353,6 +372,158 @@ class Ipv4:
         return Cursor(b.rec, b.frame, "l4", b.vlan_idx, off, self.packet_len() - self.header_len())
 
 
+class Ipv6:
+    """ipv6/generated.rs:22-216 over an IPv6 record (the record's IPv6 block,
+    include/rpkt_gpu.h); the addresses are read from the frame bytes."""
+
+    def __init__(self, buf):
+        self.buf, self.rec = buf, buf.rec
+        self.b = ip6_block(np.asarray(buf.rec).reshape(1))[0]
+
+    @staticmethod
+    def parse(buf):
+        """ipv6/generated.rs:40-51 -- Err iff chunk_len < 40 or payload_len + 40 >
+        remaining (the engine's IP6_SHORT / IP6_BAD_LEN)."""
+        rec = buf.rec
+        if (buf.stage != "l3" or buf.vlan_idx != int(rec["n_vlan"]) or not _rec_is_ip6(rec)
+                or _st(rec) in _IP6_FAIL):
+            return Err(buf)
+        return Ok(Ipv6(buf))
+
+    def version(self):
+        return int(self.b["ip6_vtcfl"]) >> 28
+
+    def traffic_class(self):
+        return (int(self.b["ip6_vtcfl"]) >> 20) & 0xff
+
+    def flow_label(self):
+        return int(self.b["ip6_vtcfl"]) & 0xfffff
+
+    def payload_len(self):
+        return int(self.b["ip6_payload_len"])
+
+    def next_header(self):
+        return int(self.b["ip6_next_header"])
+
+    def hop_limit(self):
+        return int(self.b["ip6_hop_limit"])
+
+    def _addr(self, at):
+        l3 = int(self.rec["l3_off"])
+        return ipaddress.IPv6Address(bytes(self.buf.frame[l3 + at:l3 + at + 16]))
+
+    def src_addr(self):
+        return self._addr(8)
+
+    def dst_addr(self):
+        return self._addr(24)
+
+    def payload(self):
+        """ipv6/generated.rs:83-92 -- trim to payload_len, advance 40."""
+        b = self.buf
+        return Cursor(b.rec, b.frame, "ip6ext", b.vlan_idx, b.off + 40, self.payload_len())
+
+
+class _Ip6Ext:
+    """An IPv6 extension header view over the frame bytes at a cursor (the generated
+    parse of its type; ipv6/generated.rs).  FIXED: fixed header bytes; min_len: the
+    smallest header_len its parse accepts."""
+    FIXED = 2
+    MIN_LEN = 2
+
+    def __init__(self, buf):
+        self.buf, self.rec = buf, buf.rec
+        self.h = bytes(buf.frame[buf.off:buf.off + buf.length])
+
+    @classmethod
+    def parse(cls, buf):
+        if buf.stage != "ip6ext" or buf.frame is None or buf.length < cls.FIXED:
+            return Err(buf)
+        v = cls(buf)
+        hl = v.header_len()
+        if hl < cls.MIN_LEN or hl > buf.length:
+            return Err(buf)
+        return Ok(v)
+
+    def next_header(self):
+        return self.h[0]
+
+    def header_len(self):
+        return self.h[1] * 8 + 8
+
+    def var_header_slice(self):
+        return self.h[self.FIXED:self.header_len()]
+
+    def payload(self):
+        b, hl = self.buf, self.header_len()
+        return Cursor(b.rec, b.frame, "ip6ext", b.vlan_idx, b.off + hl, b.length - hl)
+
+
+class HopByHopOption(_Ip6Ext):
+    """ipv6/generated.rs:367-421"""
+
+
+class DestOptions(_Ip6Ext):
+    """ipv6/generated.rs:224-279"""
+
+
+class RoutingHeader(_Ip6Ext):
+    """ipv6/generated.rs:511-577"""
+    FIXED = 8
+    MIN_LEN = 8
+
+    def type_(self):
+        return self.h[2]
+
+    def segments_left(self):
+        return self.h[3]
+
+    def type_specific_data(self):
+        return int.from_bytes(self.h[4:8], "big")
+
+
+class FragmentHeader(_Ip6Ext):
+    """ipv6/generated.rs:679-739"""
+    FIXED = 8
+    MIN_LEN = 8
+
+    def header_len(self):
+        return 8
+
+    def reserved(self):
+        return self.h[1]
+
+    def offset(self):
+        return int.from_bytes(self.h[2:4], "big") >> 3
+
+    def reserved1(self):
+        return (self.h[3] >> 1) & 3
+
+    def more_frag(self):
+        return bool(self.h[3] & 1)
+
+    def ident(self):
+        return int.from_bytes(self.h[4:8], "big")
+
+
+class AuthenticationHeader(_Ip6Ext):
+    """ipv6/generated.rs:833-899"""
+    FIXED = 12
+    MIN_LEN = 12
+
+    def header_len(self):
+        return self.h[1] * 4 + 8
+
+    def reserved(self):
+        return int.from_bytes(self.h[2:4], "big")
+
+    def security_parameters_index(self):
+        return int.from_bytes(self.h[4:8], "big")
+
+    def seq_num_field(self):
+        return int.from_bytes(self.h[8:12], "big")
+
+
 class _L4:
     PROTO = None
 
@@ -361,8 +532,11 @@ class _L4:
 
     @classmethod
     def parse(cls, buf):
+        """Ok where the engine's chain parsed this protocol: after Ipv4::payload(), or
+        at the cursor where the IPv6 extension headers ended (the record's l4_off)."""
         rec = buf.rec
-        if buf.stage != "l4" or _st(rec) != STATUS["OK"] or int(rec["ip_protocol"]) != cls.PROTO:
+        at_l4 = buf.stage == "l4" or (buf.stage == "ip6ext" and buf.off == int(rec["l4_off"]))
+        if not at_l4 or _st(rec) != STATUS["OK"] or int(rec["ip_protocol"]) != cls.PROTO:
             return Err(buf)
         return Ok(cls(buf))
 
@@ -393,8 +567,11 @@ class Udp(_L4):
         return int(self.rec["l4_word6"])
 
     def verify_checksum(self):
-        # smoltcp policy: a zero UDP checksum means "not computed" 
-        return self.checksum() == 0 or self.sum() == 0xffff
+        # smoltcp policy: a zero UDP checksum means "not computed" (SURVEY §8a A12), over
+        # IPv4 only (RFC 8200 section 8.1 makes it mandatory over IPv6)
+        if self.checksum() == 0 and not _rec_is_ip6(self.rec):
+            return True
+        return self.sum() == 0xffff
 
 
 class Tcp(_L4):
@@ -452,4 +629,5 @@ class Tcp(_L4):
 
 __all__ = ["EtherType", "IpProtocol", "Result", "Ok", "Err", "Cursor", "Packet",
            "EtherFrame", "EtherDot3Frame", "EtherGroup", "VlanFrame", "VlanDot3Frame",
-           "VlanGroup", "Ipv4", "Udp", "Tcp", "MAX_VLAN"]
+           "VlanGroup", "Ipv4", "Ipv6", "HopByHopOption", "DestOptions", "RoutingHeader",
+           "FragmentHeader", "AuthenticationHeader", "Udp", "Tcp", "MAX_VLAN"]

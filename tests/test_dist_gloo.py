@@ -34,6 +34,13 @@ def _worker(rank, world, port, out):
                                flow_ev=True)
     c = torch.from_numpy(oracle.flow_count(ev, NB).view(np.int64).copy())
     assert rd.reduce_counters(c) is c and rd.last_reduce_path == "gloo"
+    # the round-2 call form reduce_counters(counters, n_buckets) still works, with a warning
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        ones = torch.ones((NB + 1) * 4, dtype=torch.int64)
+        assert rd.reduce_counters(ones, NB) is ones and (ones == world).all()
+        assert any(issubclass(x.category, DeprecationWarning) for x in w)
     if rank == 0:
         np.save(out, c.numpy())
     dist.barrier()
