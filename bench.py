@@ -539,7 +539,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         t0 = time.perf_counter()
         # rpkt_gpu_flow_reduce (RCCL, C ABI) when every rank can call it, else torch's
         # all-reduce on every rank; a failure after the group chose the C ABI raises
-        rdist.reduce_counters(flow["counters"], n_buckets=nb)
+        rdist.reduce_counters(flow["counters"], n_buckets=nb, via=args.reduce_comm)
         torch.cuda.synchronize()
         red = time.perf_counter() - t0
         c = rdist.counters_as_u64(flow["counters"])
@@ -938,6 +938,9 @@ def main():
                          "fields9)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
+    ap.add_argument("--reduce-comm", default="own", choices=["own", "auto", "torch"],
+                    help="flow-counter reduce: rpkt_gpu_flow_reduce on the library's own RCCL "
+                         "communicator (own), on torch's (auto), or torch's all_reduce (torch)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
@@ -1068,6 +1071,7 @@ def main():
                        for r in [main_res] + list(extra.values()))
     if world > 1:
         dist.barrier()
+        rdist.release_own_comms()
         dist.destroy_process_group()
     if bad_counters:
         print("[bench] error: flow counters wrong after the reduce (see flow_reduce_error)",

@@ -17,6 +17,7 @@ pub const RPKT_LAYERS_BYTES: usize = 64;
 pub const RPKT_MAX_LAYERS: usize = 16;
 pub const RPKT_MAX_FIELD_REQS: u32 = 32;
 pub const RPKT_FLOW_MAX_BUCKETS: u32 = 65535;
+pub const RPKT_COLL_ID_BYTES: usize = 128;
 
 // enum rpkt_status: which rpkt `parse` returned Err first
 pub const RPKT_S_OK: u8 = 0;
@@ -265,6 +266,12 @@ extern "C" {
                                 nccl_comm: *mut c_void, stream: *mut c_void) -> c_int;
     pub fn rpkt_gpu_last_coll_error() -> c_int;
     pub fn rpkt_gpu_coll_version() -> c_int;
+    /// ncclGetUniqueId into `id_out` (RPKT_COLL_ID_BYTES bytes), on rank 0.
+    pub fn rpkt_gpu_coll_unique_id(id_out: *mut u8) -> c_int;
+    /// ncclCommInitRank on the current device; collective over `world` ranks.
+    pub fn rpkt_gpu_comm_init(comm_out: *mut *mut c_void, world: c_int, id: *const u8,
+                              rank: c_int) -> c_int;
+    pub fn rpkt_gpu_comm_destroy(comm: *mut c_void) -> c_int;
 
     pub fn rpkt_gpu_checksum_ranges(buf_dev: *const u8, buf_bytes: u64, ranges_dev: *const u32,
                                     n: u32, out_dev: *mut u16, stream: *mut c_void) -> c_int;

@@ -306,6 +306,19 @@ int rpkt_gpu_flow_reduce(uint64_t* counters_dev, uint32_t n_buckets, int root, v
 int rpkt_gpu_last_coll_error(void);
 int rpkt_gpu_coll_version(void);
 
+/* A communicator the library makes itself, so a host need not take one from another
+ * runtime (torch's ProcessGroupNCCL) for rpkt_gpu_flow_reduce: rank 0 calls
+ * rpkt_gpu_coll_unique_id (ncclGetUniqueId) and hands the RPKT_COLL_ID_BYTES bytes to
+ * every rank by any channel (the reference's receive threads share memory; ranks of
+ * one host here use the torch group, an MPI broadcast or a file), then every rank
+ * calls rpkt_gpu_comm_init (ncclCommInitRank on its current HIP device; collective:
+ * it returns when all `world` ranks have joined) and, when done,
+ * rpkt_gpu_comm_destroy.  *comm_out is an ncclComm_t as void*. */
+#define RPKT_COLL_ID_BYTES 128
+int rpkt_gpu_coll_unique_id(uint8_t* id_out);
+int rpkt_gpu_comm_init(void** comm_out, int world, const uint8_t* id, int rank);
+int rpkt_gpu_comm_destroy(void* comm);
+
 /* Batched checksum::from_slice over byte ranges of a device buffer:
  * out_dev[i] = from_slice(buf[start_i .. start_i + len_i]) for
  * ranges_dev[i] = {start_i, len_i}.  Drop-in for rpkt/src/checksum.rs:33-62. */

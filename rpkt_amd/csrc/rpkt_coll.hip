@@ -27,8 +27,12 @@ struct Rccl {
     decltype(&ncclCommCount) comm_count = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
     bool ok = false;
 };
+static_assert(sizeof(ncclUniqueId) == RPKT_COLL_ID_BYTES, "RCCL unique id size");
 
 const Rccl& rccl() {
     static Rccl R;
@@ -42,7 +46,11 @@ const Rccl& rccl() {
         R.comm_count = (decltype(R.comm_count))dlsym(h, "ncclCommCount");
         R.all_reduce = (decltype(R.all_reduce))dlsym(h, "ncclAllReduce");
         R.reduce = (decltype(R.reduce))dlsym(h, "ncclReduce");
-        R.ok = R.get_version && R.comm_count && R.all_reduce && R.reduce;
+        R.get_unique_id = (decltype(R.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        R.comm_init_rank = (decltype(R.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        R.comm_destroy = (decltype(R.comm_destroy))dlsym(h, "ncclCommDestroy");
+        R.ok = R.get_version && R.comm_count && R.all_reduce && R.reduce && R.get_unique_id &&
+               R.comm_init_rank && R.comm_destroy;
     });
     return R;
 }
@@ -56,6 +64,56 @@ int rpkt_gpu_coll_version(void) {
     const Rccl& R = rccl();
     int v = 0;
     return R.ok && R.get_version(&v) == ncclSuccess ? v : -1;
+}
+
+// ---- a communicator the library owns (the caller does not need one from elsewhere) ----
+int rpkt_gpu_coll_unique_id(uint8_t* id_out) {
+    if (!id_out) return RPKT_E_INVAL;
+    const Rccl& R = rccl();
+    if (!R.ok) {
+        g_last_coll_error = (int)ncclSystemError;
+        return RPKT_E_COLL;
+    }
+    ncclUniqueId id;
+    const ncclResult_t r = R.get_unique_id(&id);
+    if (r != ncclSuccess) {
+        g_last_coll_error = (int)r;
+        return RPKT_E_COLL;
+    }
+    memcpy(id_out, &id, sizeof(id));
+    return RPKT_OK;
+}
+
+int rpkt_gpu_comm_init(void** comm_out, int world, const uint8_t* id, int rank) {
+    if (!comm_out || !id || world < 1 || rank < 0 || rank >= world) return RPKT_E_INVAL;
+    *comm_out = nullptr;
+    const Rccl& R = rccl();
+    if (!R.ok) {
+        g_last_coll_error = (int)ncclSystemError;
+        return RPKT_E_COLL;
+    }
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = R.comm_init_rank(&comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        g_last_coll_error = (int)r;
+        return RPKT_E_COLL;
+    }
+    *comm_out = comm;
+    return RPKT_OK;
+}
+
+int rpkt_gpu_comm_destroy(void* comm) {
+    if (!comm) return RPKT_E_INVAL;
+    const Rccl& R = rccl();
+    if (!R.ok) return RPKT_E_COLL;
+    const ncclResult_t r = R.comm_destroy((ncclComm_t)comm);
+    if (r != ncclSuccess) {
+        g_last_coll_error = (int)r;
+        return RPKT_E_COLL;
+    }
+    return RPKT_OK;
 }
 
 int rpkt_gpu_flow_reduce(uint64_t* counters_dev, uint32_t n_buckets, int root, void* nccl_comm,

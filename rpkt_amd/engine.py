@@ -58,7 +58,9 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_flow_reduce", "rpkt_gpu_last_coll_error", "rpkt_gpu_coll_version",
            "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact",
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
-           "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact"]
+           "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact", "rpkt_gpu_coll_unique_id",
+           "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy"]
+COLL_ID_BYTES = 128
 
 _lib = None
 
@@ -142,6 +144,13 @@ def lib():
         L.rpkt_gpu_flow_reduce.restype = ctypes.c_int
         L.rpkt_gpu_last_coll_error.restype = ctypes.c_int
         L.rpkt_gpu_coll_version.restype = ctypes.c_int
+        L.rpkt_gpu_coll_unique_id.argtypes = [ctypes.c_void_p]
+        L.rpkt_gpu_coll_unique_id.restype = ctypes.c_int
+        L.rpkt_gpu_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_int]
+        L.rpkt_gpu_comm_init.restype = ctypes.c_int
+        L.rpkt_gpu_comm_destroy.argtypes = [ctypes.c_void_p]
+        L.rpkt_gpu_comm_destroy.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -344,6 +353,28 @@ def nccl_comm_of(group=None):
         return None
     ptr = int(g._get_backend(torch.device("cuda", torch.cuda.current_device()))._comm_ptr())
     return ptr or None
+
+
+def coll_unique_id():
+    """rpkt_gpu_coll_unique_id: a fresh RCCL unique id (bytes) for rpkt_gpu_comm_init."""
+    buf = (ctypes.c_uint8 * COLL_ID_BYTES)()
+    _check(lib().rpkt_gpu_coll_unique_id(buf), "rpkt_gpu_coll_unique_id")
+    return bytes(buf)
+
+
+def comm_init(world, uid, rank):
+    """rpkt_gpu_comm_init on the current device: the library's own ncclComm_t (as int).
+    Collective: returns when all `world` ranks have called it with the same id."""
+    if len(uid) != COLL_ID_BYTES:
+        raise RpktError("comm_init: the id must be %d bytes" % COLL_ID_BYTES)
+    buf = (ctypes.c_uint8 * COLL_ID_BYTES).from_buffer_copy(uid)
+    comm = ctypes.c_void_p()
+    _check(lib().rpkt_gpu_comm_init(ctypes.byref(comm), world, buf, rank), "rpkt_gpu_comm_init")
+    return int(comm.value)
+
+
+def comm_destroy(comm):
+    _check(lib().rpkt_gpu_comm_destroy(ctypes.c_void_p(int(comm))), "rpkt_gpu_comm_destroy")
 
 
 def checksum_ranges(buf, ranges, out=None, stream=None):

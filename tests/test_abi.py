@@ -175,9 +175,13 @@ def test_ring_argument_validation_without_launch(L):
     assert L.rpkt_gpu_parse_ring(None, 0, 3, 0, None) == 0                    # nothing to do
     assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == 0                       # all n == 0
     assert L.rpkt_gpu_parse_ring(P, 3, 0x80, 0, None) == -1                   # bad flag
-    assert L.rpkt_gpu_parse_ring(P, 3, 7, 0, None) == -1                      # FLOW_EV, 0 buckets
+    # FLOW_EV with 0 buckets: nothing to do for empty slots (as parse_batch with n == 0)
+    assert L.rpkt_gpu_parse_ring(P, 3, 7, 0, None) == 0
     S[1].batch = engine.Batch(4096, 640, None, 64, 0, 10, 0)
     S[1].recs_dev = 16
+    S[1].flow_ev_dev = 64
+    assert L.rpkt_gpu_parse_ring(P, 3, 7, 0, None) == -1                      # FLOW_EV, 0 buckets
+    S[1].flow_ev_dev = None
     S[2].batch = engine.Batch(4096, 1 << 32, None, 64, 0, 10, 0)
     S[2].recs_dev = 16
     assert L.rpkt_gpu_parse_ring(P, 3, 3, 0, None) == -3                      # slot 2 > 4 GiB

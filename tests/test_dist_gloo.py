@@ -91,3 +91,31 @@ def test_reduce_path_is_decided_for_the_whole_group(tmp_path, flags):
     mp.spawn(_agree_worker, args=(world, _free_port(), flags, out), nprocs=world, join=True)
     got = {open("%s.%d" % (out, r)).read() for r in range(world)}
     assert got == {"1" if all(flags) else "0"}
+
+
+def _id_worker(rank, world, port, fail, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rpkt_amd import dist as rd
+
+    def make_id():                       # stands in for rpkt_gpu_coll_unique_id (rank 0 only)
+        assert rank == 0
+        if fail:
+            raise RuntimeError("no RCCL")
+        return bytes(range(128))
+    got = rd.exchange_id(make_id)
+    with open("%s.%d" % (out, rank), "wb") as fh:
+        fh.write(b"NONE" if got is None else got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail", [(2, False), (3, False), (2, True)])
+def test_own_communicator_id_exchange(tmp_path, world, fail):
+    """The library-owned communicator's id (dist.exchange_id): rank 0 makes it, every rank
+    receives the same 128 bytes; when rank 0 cannot make one every rank gets None (no rank
+    goes on to rpkt_gpu_comm_init alone)."""
+    out = str(tmp_path / "id")
+    mp.spawn(_id_worker, args=(world, _free_port(), fail, out), nprocs=world, join=True)
+    got = {open("%s.%d" % (out, r), "rb").read() for r in range(world)}
+    assert got == {b"NONE" if fail else bytes(range(128))}

@@ -169,3 +169,46 @@ def test_flow_count_from_two_host_threads(tmp_path):
                        timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "threads ok" in r.stdout
+
+
+OWN_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, %r)
+import numpy as np, torch, torch.distributed as dist
+from rpkt_amd import dist as rd, engine
+torch.cuda.set_device(0)
+# the library's own communicator through the C ABI alone (no torch group)
+uid = engine.coll_unique_id()
+assert len(uid) == engine.COLL_ID_BYTES and any(uid)
+comm = engine.comm_init(1, uid, 0)
+nb = 4096
+rng = np.random.default_rng(6)
+host = rng.integers(0, 2**62, (nb + 1) * 4, dtype=np.int64)
+c = torch.from_numpy(host.copy()).cuda()
+engine.flow_reduce(c, nb, comm)
+torch.cuda.synchronize()
+assert np.array_equal(c.cpu().numpy(), host)
+engine.comm_destroy(comm)
+# and as the dist path makes it: id from rank 0, broadcast over the torch group
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=%r, RANK="0", WORLD_SIZE="1")
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+comm2, why = rd.own_comm()
+assert comm2 and why is None, why
+engine.flow_reduce(c, nb, comm2, root=0)
+torch.cuda.synchronize()
+assert np.array_equal(c.cpu().numpy(), host)
+rd.release_own_comms()
+dist.destroy_process_group()
+print("own comm ok")
+"""
+
+
+def test_flow_reduce_on_the_library_own_communicator(tmp_path):
+    """rpkt_gpu_coll_unique_id + rpkt_gpu_comm_init (world 1) + rpkt_gpu_flow_reduce +
+    rpkt_gpu_comm_destroy, directly and through dist.own_comm over an RCCL group."""
+    script = tmp_path / "own.py"
+    script.write_text(OWN_SCRIPT % (ROOT, str(_free_port())))
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True,
+                       timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "own comm ok" in r.stdout
