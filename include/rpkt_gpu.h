@@ -459,6 +459,24 @@ typedef struct rpkt_opts {
 
 #define RPKT_OPTS_BYTES 64u
 
+/* IPv6 frames (records of an RPKT_F_IPV6 parse): TcpOptionsIter as for IPv4, and in
+ * place of the IPv4 walk, Ipv6OptionsIter (ipv6/generated.rs:1556-1615) over the
+ * var_header_slice() of every HopByHopOption / DestOptions header of the extension chain
+ * the parse walked ([l3 + 40, l4)), in order (ipv6_test.rs:47-69, 154-175); a malformed
+ * option ends the walking.  Kinds (bits of ip_kinds, codes index + 1 in ip_trace):
+ * 0 Pad0, 1 PadN, 2 RouterAlert, 3 Generic (every other type).  The IPv6 view of bytes
+ * 27..47:
+ *   27 ip_end          bytes consumed in the last header walked
+ *   28 ip_count        options yielded over every header walked
+ *   29 ip_stop         NONE (no options header), END, or MALFORMED
+ *   30 ip_kinds
+ *   32 ip_route_alert  RouterAlert::router_alert (the last one)
+ *   34 u8 generic type / 35 u8 generic data length: Generic::type_ and header_len - 2
+ *   36 u8 option headers walked / 37 u8 the first one's type (0 HopByHop, 60 DestOptions)
+ *   40 u32 generic data: the first <= 4 bytes of that Generic's var_header_slice(),
+ *          big-endian, zero-filled (ipv6_test.rs:54)
+ * other bytes of the half are 0. */
+
 /* Walk the IPv4 and TCP options of every frame of a parsed batch: recs_dev from
  * rpkt_gpu_parse_batch on the same batch locates the slices (ip: [l3 + 20, l4),
  * tcp: [l4 + 20, payload_off) for status OK / TCP).  opts_dev n * 64 B, 16-B aligned. */

@@ -59,6 +59,69 @@ static int ip_opt(const uint8_t* b, uint32_t n, int* kind) {
     }
 }
 
+int oracle_rec_is_ip6(const rpkt_rec_t* r);       /* rpkt_oracle.c */
+
+/* Ipv6OptionsIter::next (rpkt/src/ipv6/generated.rs:1568-1615): the first byte picks the
+ * option; Pad0 (0) is one byte (:1446-1453); PadN (1, :1302-1313) and Generic (2..4,
+ * 6..255, :1017-1028): chunk >= 2 and 2 <= header_len = b1 + 2 <= chunk; RouterAlert
+ * (5, :1160-1171): chunk >= 4 and header_len == 4.  Every type is some option, so the
+ * walk stops only at the slice's end or at a failed parse.  Returns the bytes the
+ * option takes, 0 = malformed; *kind = 0 Pad0, 1 PadN, 2 RouterAlert, 3 Generic. */
+static int ip6_opt(const uint8_t* b, uint32_t n, int* kind) {
+    uint32_t t = b[0];
+    if (t == 0) { *kind = 0; return 1; }
+    *kind = t == 1 ? 1 : (t == 5 ? 2 : 3);
+    if (t == 5) return (n >= 4 && b[1] + 2u == 4) ? 4 : 0;
+    if (n < 2) return 0;
+    uint32_t hl = b[1] + 2u;                          /* header_len :1328-1330, :1043-1045 */
+    return hl <= n ? (int)hl : 0;
+}
+
+/* The IPv6 half of rpkt_opts_t (include/rpkt_gpu.h): Ipv6OptionsIter over the
+ * var_header_slice() (bytes [2, header_len)) of every HopByHopOption / DestOptions header
+ * of the chain the parse walked (frame bytes [l3 + 40, l4_off)), in order, as a receive
+ * loop walks them (ipv6_test.rs:47-69, 154-175); a malformed option ends the walking. */
+static void ip6_options(const uint8_t* f, const rpkt_rec_t* r, rpkt_opts_t* o) {
+    if (r->status == RPKT_S_IP6_SHORT || r->status == RPKT_S_IP6_BAD_LEN) return;
+    uint32_t c = r->l3_off + 40u, l4 = r->l4_off;
+    uint32_t nh = f[r->l3_off + 6];
+    uint8_t* ip = (uint8_t*)o + 27;                   /* bytes 27..47: the IPv6 view */
+    uint32_t count = 0;                               /* stored as u8 (ip_count) */
+    for (int k = 0; k < RPKT_MAX_IP6_EXT && c < l4; k++) {
+        const uint8_t* h = f + c;
+        uint32_t hl = nh == 44 ? 8u : (nh == 51 ? h[1] * 4u + 8u : h[1] * 8u + 8u);
+        if (nh == 0 || nh == 60) {
+            if (ip[9] == 0) ip[10] = (uint8_t)nh;     /* ip6_first_hdr (byte 37) */
+            ip[9]++;                                  /* ip6_opt_hdrs  (byte 36) */
+            const uint8_t* b = h + 2;                 /* var_header_slice :258-261, :401-404 */
+            uint32_t n = hl - 2, pos = 0;
+            o->ip_stop = RPKT_OPT_END;
+            while (pos < n) {
+                int kind = 0, used = ip6_opt(b + pos, n - pos, &kind);
+                if (used == 0) { o->ip_stop = RPKT_OPT_MALFORMED; break; }
+                const uint8_t* p = b + pos;
+                if (kind == 2) o->ip_route_alert = be16(p + 2);          /* :1181-1183 */
+                if (kind == 3) {                                          /* :1039-1045 */
+                    uint32_t dl = p[1], v = 0;
+                    for (uint32_t q = 0; q < 4; q++) v = (v << 8) | (q < dl ? p[2 + q] : 0u);
+                    ip[7] = p[0];                     /* ip6_generic_type (byte 34) */
+                    ip[8] = p[1];                     /* ip6_generic_len  (byte 35) */
+                    o->ip_sr_dest = v;                /* ip6_generic_data (bytes 40..43) */
+                }
+                o->ip_kinds |= (uint16_t)(1u << kind);
+                if (count < 16) o->ip_trace |= (uint64_t)(kind + 1) << (4 * count);
+                count++;
+                pos += (uint32_t)used;
+            }
+            o->ip_count = (uint8_t)count;
+            o->ip_end = (uint8_t)pos;
+            if (o->ip_stop == RPKT_OPT_MALFORMED) break;
+        }
+        nh = h[0];
+        c += hl;
+    }
+}
+
 void oracle_options_one(const uint8_t* f, uint32_t len, const rpkt_rec_t* r, rpkt_opts_t* o) {
     memset(o, 0, sizeof(*o));
     (void)len;
@@ -85,6 +148,7 @@ void oracle_options_one(const uint8_t* f, uint32_t len, const rpkt_rec_t* r, rpk
         }
         o->ip_end = (uint8_t)pos;
     }
+    if (oracle_rec_is_ip6(r)) ip6_options(f, r, o);
     if (r->status == RPKT_S_OK && r->ip_protocol == 6) {
         uint32_t doff4 = (uint32_t)(r->l4_word6 >> 12) * 4;
         const uint8_t* b = f + r->l4_off + 20;

@@ -138,6 +138,8 @@ struct OptSlices {
     uint32_t ip_lo, ip_hi, t_lo, t_hi;
     uint32_t need_lo, need_hi;     // frame bytes both walks read: [need_lo, need_hi)
     bool need;
+    bool ip6;                      // IPv6 header parsed: the IPv6 option walk (ip6_walk_row)
+    uint32_t l3, l4;               //   over the extension chain [l3 + 40, l4)
 };
 
 // is6: an IPv6 record (RPKT_F_IPV6): no IPv4 option slice; its TCP slice as any other
@@ -154,7 +156,96 @@ __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto,
     S.need_lo = S.ip_hi > S.ip_lo ? S.ip_lo : S.t_lo;
     S.need_hi = S.t_hi > S.t_lo ? S.t_hi : S.ip_hi;
     S.need = (S.ip_hi > S.ip_lo) || (S.t_hi > S.t_lo);
+    S.ip6 = is6 && status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN;
+    S.l3 = l3;
+    S.l4 = l4;
     return S;
+}
+
+// ---- Ipv6OptionsIter over the extension chain (the IPv6 half of rpkt_opts_t) ----
+// Ipv6OptionsIter::next (ipv6/generated.rs:1568-1615) over the var_header_slice() of every
+// HopByHopOption / DestOptions header (:384-412, :241-269) of the chain the parse walked,
+// frame bytes [l3 + 40, l4), in order; a malformed option ends the walking.  Pad0 (0) is
+// one byte; PadN (1) and Generic (2..4, 6..255): chunk >= 2 and header_len = b1 + 2 <=
+// chunk; RouterAlert (5): chunk >= 4 and header_len == 4.  A lane walks its own frame from
+// global memory (the bytes were just fetched by the window or the refill, so mostly L2
+// hits): the chain can run far past the 128-B window (a HopByHop header alone may hold
+// 2048 B), and few frames carry options headers.  Writes words 7..11, 14, 15 and byte 27
+// of the frame's 64-B row (include/rpkt_gpu.h, the IPv6 view).
+__device__ __forceinline__ uint32_t gdword(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t a) {
+    const uint32_t a4 = a & ~3u;
+    auto ld = [&](uint32_t x) -> uint32_t {
+        if (__builtin_expect(x + 4u <= fb, 1))
+            return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)x, 0, 0);
+        return gbyte(rs, x) | (gbyte(rs, x + 1u) << 8) | (gbyte(rs, x + 2u) << 16) |
+               (gbyte(rs, x + 3u) << 24);      // the buffer's last, partial dword
+    };
+    return align_bytes(ld(a4 + 4u), ld(a4), a & 3u);
+}
+
+__device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t fo,
+                                             uint32_t l3, uint32_t l4, uint32_t* row) {
+    uint32_t nh = (gdword(rs, fb, fo + l3 + 4u) >> 16) & 0xffu;   // next_header, byte 6
+    uint32_t c = l3 + 40u;
+    uint32_t cnt = 0, kinds = 0, stop = RPKT_OPT_NONE, end = 0, ra = 0, gt = 0, gl = 0, gd = 0;
+    uint32_t nhdr = 0, first = 0;
+    uint64_t trace = 0;
+    for (int k = 0; k < RPKT_MAX_IP6_EXT && c < l4; ++k) {
+        const uint32_t d0 = gdword(rs, fb, fo + c);
+        const uint32_t b1 = (d0 >> 8) & 0xffu;
+        const uint32_t hl = nh == 44u ? 8u : (nh == 51u ? b1 * 4u + 8u : b1 * 8u + 8u);
+        if (nh == 0u || nh == 60u) {
+            first = nhdr == 0u ? nh : first;
+            nhdr += 1u;
+            stop = RPKT_OPT_END;
+            const uint32_t s0 = c + 2u, nb = hl - 2u;
+            uint32_t pos = 0;
+            while (pos < nb) {
+                const uint32_t d = gdword(rs, fb, fo + s0 + pos);
+                const uint32_t t = d & 0xffu, rem = nb - pos;
+                if (t == 0u) {                          // a run of Pad0 (up to 4 bytes)
+                    uint32_t kz = d ? (uint32_t)__builtin_ctz(d) >> 3 : 4u;
+                    kz = kz < rem ? kz : rem;
+                    kinds |= 1u;
+                    trace |= cnt < 16u ? (uint64_t)(0x1111u & ((1u << (4u * kz)) - 1u)) << (4u * cnt)
+                                       : 0ull;
+                    cnt += kz;
+                    pos += kz;
+                    continue;
+                }
+                const uint32_t ln = ((d >> 8) & 0xffu) + 2u;             // header_len
+                const bool ok = t == 5u ? (rem >= 4u && ln == 4u) : (rem >= 2u && ln <= rem);
+                if (!ok) {
+                    stop = RPKT_OPT_MALFORMED;
+                    break;
+                }
+                const uint32_t kind = t == 1u ? 1u : (t == 5u ? 2u : 3u);
+                if (kind == 2u) ra = be16_hi(d);                         // router_alert
+                if (kind == 3u) {                                        // Generic: type_,
+                    gt = t;                                              // data length, the
+                    gl = ln - 2u;                                        // slice's first bytes
+                    const uint32_t v = bswap32(gdword(rs, fb, fo + s0 + pos + 2u));
+                    gd = gl >= 4u ? v : v & ~(0xffffffffu >> (8u * gl));
+                }
+                kinds |= 1u << kind;
+                trace |= cnt < 16u ? (uint64_t)(kind + 1u) << (4u * cnt) : 0ull;
+                cnt += 1u;
+                pos += ln;
+            }
+            end = pos;
+            if (stop == RPKT_OPT_MALFORMED) break;
+        }
+        nh = d0 & 0xffu;
+        c += hl;
+    }
+    row[7] = (cnt & 0xffu) | (stop << 8) | (kinds << 16);
+    row[8] = ra | (gt << 16) | (gl << 24);
+    row[9] = nhdr | (first << 8);
+    row[10] = gd;
+    row[11] = 0u;
+    row[14] = (uint32_t)trace;
+    row[15] = (uint32_t)(trace >> 32);
+    reinterpret_cast<uint8_t*>(row)[27] = (uint8_t)end;
 }
 
 // The two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
@@ -241,6 +332,17 @@ __device__ __forceinline__ void walk_options(const OptWin& s, const OptSlices& S
     o[15] = (uint32_t)(ip_trace >> 32);
 }
 
+// The IPv6 half of one frame's row staged in LDS (`row`, 17-dword stride), for lanes whose
+// frame is IPv6; the wave synchronises before and after (other lanes wrote the rows).
+__device__ __forceinline__ void ip6_patch_rows(uint32_t* st, int lane, const OptSlices& S,
+                                               __amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                               uint32_t fo) {
+    if (__ballot(S.ip6) == 0) return;                          // wave-uniform
+    wave_sync();
+    if (S.ip6) ip6_walk_row(rs, fb, fo, S.l3, S.l4, st + lane * 17);
+    wave_sync();
+}
+
 // ---- paired walks: one iterator step per lane per iteration ----
 // walk_options steps a frame's two walks together, so every loop iteration runs both
 // step bodies and a wave runs until its longest walk of either kind ends (config 5: 14.1
@@ -281,7 +383,9 @@ struct OptCur {
 // the stage rows (stride 17 dwords) in `win` once every walk of the wave has ended.
 __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint32_t slot_bias,
                                                     const OptSlices& S, const uint8_t* rules,
-                                                    rpkt_opts_t* opts, uint32_t p0, uint32_t n) {
+                                                    rpkt_opts_t* opts, uint32_t p0, uint32_t n,
+                                                    __amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                    uint32_t fo) {
     // (a lane past the batch end may hold a zero record: status OK, l4 = 0, so a slice
     // can come out "negative"; it is empty, as walk_options' `on` flags treat it)
     const uint32_t t_nb = S.tcp && S.t_hi > S.t_lo ? S.t_hi - S.t_lo : 0u;
@@ -590,6 +694,7 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
     pq[14] = o[14]; pq[15] = o[15];
     reinterpret_cast<uint8_t*>(pq)[27] = (uint8_t)ip_end;
     wave_sync();
+    ip6_patch_rows(st, lane, S, rs, fb, fo);                   // IPv6 frames' option walks
     const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
 #pragma unroll
@@ -604,11 +709,14 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
 // stored as 64-B rows, 4 KiB coalesced, with non-temporal stores.  `st` must not be
 // read by any lane of the wave after this call begins until it returns.
 __device__ __forceinline__ void store_opts(uint32_t* st, int lane, const uint32_t (&o)[16],
-                                           rpkt_opts_t* opts, uint32_t p0, uint32_t n) {
+                                           rpkt_opts_t* opts, uint32_t p0, uint32_t n,
+                                           const OptSlices& S, __amdgpu_buffer_rsrc_t rs,
+                                           uint32_t fb, uint32_t fo) {
     wave_sync();
 #pragma unroll
     for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
     wave_sync();
+    ip6_patch_rows(st, lane, S, rs, fb, fo);
     const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
 #pragma unroll

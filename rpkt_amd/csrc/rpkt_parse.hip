@@ -61,14 +61,14 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
     }
 #if RPKT_OPT_ABLATE == 1
     uint32_t o[16] = {};
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
 #elif RPKT_OPT_PAIRED
-    walk_options_paired(W.win, lane, lane * kSlot + bias, S, rules, opts, p0, n);
+    walk_options_paired(W.win, lane, lane * kSlot + bias, S, rules, opts, p0, n, rs, fb, fr.off);
 #else
     const OptWin s{&W.win[lane * kSlot], bias};
     uint32_t o[16];
     walk_options(s, S, rules, o);
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
 #endif
 }
 

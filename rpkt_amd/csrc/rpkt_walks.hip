@@ -135,12 +135,12 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 
 #if RPKT_OPT_PAIRED
     walk_options_paired(W.win, lane, lane * kOptSlot + (((fr.off + need_lo) & 15u) - need_lo), S,
-                        rules, opts, p0, n);
+                        rules, opts, p0, n, rs, fb, fr.off);
 #else
     const OptWin s{&W.win[lane * kOptSlot], ((fr.off + need_lo) & 15u) - need_lo};
     uint32_t o[16];
     walk_options(s, S, rules, o);
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
 #endif
 }
 

@@ -114,6 +114,18 @@ OPTS_DTYPE = np.dtype([          # rpkt_opts_t (include/rpkt_gpu.h), 64 B
 ])
 assert OPTS_DTYPE.itemsize == OPTS_BYTES
 OPT_STOP = {"NONE": 0, "END": 1, "UNKNOWN": 2, "MALFORMED": 3}
+IP6_OPT_KINDS = ("Pad0", "Padn", "RouterAlert", "Generic")
+IP6_OPTS_DTYPE = np.dtype([      # rpkt_opts_t bytes 27..47 of an IPv6 frame (include/rpkt_gpu.h)
+    ("end", "u1"), ("count", "u1"), ("stop", "u1"), ("kinds", "<u2"), ("router_alert", "<u2"), ("generic_type", "u1"), ("generic_len", "u1"), ("n_hdrs", "u1"),
+    ("first_hdr", "u1"), ("pad1", "u1", (2,)), ("generic_data", "<u4"), ("pad2", "u1", (4,)),
+])
+assert IP6_OPTS_DTYPE.itemsize == 21
+
+
+def ip6_opts_view(opts):
+    """The IPv6 option-walk view of rpkt_opts_t records (bytes 27..47; trace: ip_trace)."""
+    raw = np.ascontiguousarray(opts).view(np.uint8).reshape(-1, OPTS_BYTES)[:, 27:48]
+    return np.ascontiguousarray(raw).view(IP6_OPTS_DTYPE).reshape(-1)
 TCP_KINDS = ("Eol", "Nop", "Mss", "WindowScale", "SackPermitted", "Sack", "Timestamp", "FastOpen")
 IP_KINDS = ("Eol", "Nop", "Timestamp", "RecordRoute", "RouteAlert", "CommercialSecurity",
             "StrictSourceRoute", "LooseSourceRoute")

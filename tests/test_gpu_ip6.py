@@ -92,7 +92,30 @@ def test_fixtures_every_alignment_ip6(torch, lead):
     assert int(r["status"]) == STATUS["IP6_FRAGMENT"]
 
 
-def _ip6_frame(rng, exts, proto, payload, tag=False):
+def _ip6_opts(rng, n, bad=False):
+    """n bytes of IPv6 options (Pad0 / PadN / RouterAlert / Generic), optionally ending in
+    a malformed one."""
+    out = bytearray()
+    while len(out) < n:
+        left = n - len(out)
+        k = int(rng.integers(0, 4))
+        if k == 1 and left >= 4:
+            out += bytes([5, 2]) + int(rng.integers(0, 3)).to_bytes(2, "big")
+        elif k == 2 and left >= 3:
+            dl = int(min(left - 2, rng.integers(1, 9)))
+            out += bytes([int(rng.choice([2, 11, 0xc2])), dl]) + \
+                rng.integers(0, 256, dl, dtype=np.uint8).tobytes()
+        elif k == 3 and left >= 2:
+            dl = int(min(left - 2, rng.integers(0, 6)))
+            out += bytes([1, dl]) + bytes(dl)
+        else:
+            out += b"\x00"
+    if bad and n >= 2:
+        out[-2:] = bytes([11, 9])                      # header_len past the slice
+    return bytes(out)
+
+
+def _ip6_frame(rng, exts, proto, payload, tag=False, opts=False):
     """Ether [+ 802.1Q] + IPv6 + extension headers (type, header_len) + UDP/TCP + payload
     bytes; the L4 checksum is stamped valid with the pseudo header over the final address."""
     f = bytearray(b"\x02\x00\x00\x00\x00\x01\x02\x00\x00\x00\x00\x02")
@@ -111,7 +134,8 @@ def _ip6_frame(rng, exts, proto, payload, tag=False):
         if t in (0, 60, 43):
             h[1] = hl // 8 - 1
         if t in (0, 60):
-            h[2:hl] = bytes(hl - 2)                                      # Pad1 options
+            h[2:hl] = (_ip6_opts(rng, hl - 2, bad=rng.integers(0, 8) == 0) if opts
+                       else bytes(hl - 2))                               # Pad0 options
         if t == 43:
             h[2], h[3] = 0, 1                                            # type 0, 1 left
             n = (hl - 8) // 16
@@ -248,3 +272,19 @@ def test_short_strided_ip6_frames(torch):
             k = min(int(lens[i]), flen)
             buf[i * stride:i * stride + k] = src.frames[a:a + k]
         check_batch(gen.HostBatch(12, src.n, 0, buf, None, stride, flen))
+
+
+@pytest.mark.parametrize("lead", [0, 1, 5, 11])
+def test_ip6_option_walks_fixtures_and_long_chains(torch, lead):
+    """Ipv6OptionsIter over every HopByHop / DestOptions header (the IPv6 half of
+    rpkt_opts_t): the captures, and crafted chains whose options headers run past the
+    window (up to 2048 B), with PadN / RouterAlert / Generic options and malformed ones."""
+    rng = np.random.default_rng(71 + lead)
+    _, frames = fixtures()
+    for hbh in (8, 24, 64, 160, 512, 2048):
+        for tail in ([], [(60, 16)], [(43, 40), (60, 24)], [(44, 8), (60, 8), (60, 16)]):
+            pl = rng.integers(0, 256, int(rng.integers(0, 600)), dtype=np.uint8).tobytes()
+            frames.append(_ip6_frame(rng, [(0, hbh)] + tail, int(rng.choice([6, 17])), pl,
+                                     opts=True))
+    hb = host_batch(frames, lead)
+    _opts_check(engine.DeviceBatch.from_host(hb), hb, F6)

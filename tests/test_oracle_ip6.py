@@ -16,7 +16,8 @@ import pytest
 
 from oracle import oracle
 from rpkt_amd import gen
-from rpkt_amd.records import STATUS, F_IPV6, ip6_block, is_ip6, project16, MAX_IP6_EXT
+from rpkt_amd.records import (STATUS, F_IPV6, OPT_STOP, IP6_OPT_KINDS, ip6_block, ip6_opts_view,
+                              is_ip6, project16, trace_kinds, MAX_IP6_EXT)
 from rpkt_amd.views import (EtherFrame, Ipv4, Ipv6, DestOptions, HopByHopOption, RoutingHeader,
                             FragmentHeader, AuthenticationHeader, Udp, Packet, EtherType,
                             IpProtocol)
@@ -323,3 +324,87 @@ def test_ipv4_view_refuses_ip6_record():
     rec = oracle.parse_one(frame, FLAGS6)
     eth = EtherFrame.parse(Packet(rec, frame)).unwrap()
     assert Ipv4.parse(eth.payload()).is_err()
+
+
+# ---- Ipv6OptionsIter (the IPv6 half of rpkt_opts_t) ----
+
+def opts_of(name):
+    f = load(name)
+    r = np.array([oracle.parse_one(f, FLAGS6)])
+    o = oracle.options_batch(np.frombuffer(f, dtype=np.uint8), 1, r,
+                             offsets=np.array([0, len(f)], dtype=np.uint32))
+    return o[0], ip6_opts_view(o)[0]
+
+
+def test_ip6_options_destination():
+    """ipv6_test.rs:47-69: Generic (type 11, header_len 3, var_header_slice()[0] == 9),
+    then PadN (header_len 3, var_header_slice()[0] == 0), then None."""
+    o, v = opts_of("ipv6_options_destination.dat")
+    assert trace_kinds(o["ip_trace"], o["ip_count"], IP6_OPT_KINDS) == ["Generic", "Padn"]
+    assert int(v["stop"]) == OPT_STOP["END"] and int(v["end"]) == 6        # 3 + 3 bytes
+    assert (int(v["generic_type"]), int(v["generic_len"]) + 2) == (11, 3)
+    assert int(v["generic_data"]) >> 24 == 9
+    assert (int(v["n_hdrs"]), int(v["first_hdr"])) == (1, 60)
+    assert int(o["tcp_stop"]) == OPT_STOP["NONE"]                          # UDP
+
+
+def test_ip6_options_hop_by_hop():
+    """ipv6_test.rs:154-175: RouterAlert (type 5, header_len 4, router_alert 0), then PadN
+    (header_len 2), then None."""
+    o, v = opts_of("ipv6_options_hop_by_hop.dat")
+    assert trace_kinds(o["ip_trace"], o["ip_count"], IP6_OPT_KINDS) == ["RouterAlert", "Padn"]
+    assert int(v["router_alert"]) == 0 and int(v["end"]) == 6              # 4 + 2 bytes
+    assert int(v["stop"]) == OPT_STOP["END"] and (int(v["n_hdrs"]), int(v["first_hdr"])) == (1, 0)
+
+
+def test_ip6_options_every_options_header():
+    """ipv6_options_multi.dat: HopByHop then DestOptions are both walked, in order."""
+    o, v = opts_of("ipv6_options_multi.dat")
+    assert trace_kinds(o["ip_trace"], o["ip_count"], IP6_OPT_KINDS) == \
+        ["RouterAlert", "Padn", "Generic", "Padn"]
+    assert (int(v["n_hdrs"]), int(v["first_hdr"])) == (2, 0)
+    o, v = opts_of("ipv6_options_routing1.dat")                           # no options header
+    assert int(v["stop"]) == OPT_STOP["NONE"] and int(o["ip_count"]) == 0
+
+
+def model_ip6_opts(f, l3, l4):
+    """Independent Python restatement of the walk (ipv6/generated.rs:1568-1615)."""
+    c, nh, out, stop, hdrs = l3 + 40, f[l3 + 6], [], 0, 0
+    for _ in range(MAX_IP6_EXT):
+        if c >= l4:
+            break
+        hl = 8 if nh == 44 else (f[c + 1] * 4 + 8 if nh == 51 else f[c + 1] * 8 + 8)
+        if nh in (0, 60):
+            hdrs += 1
+            b, pos, stop = f[c + 2:c + hl], 0, 1
+            while pos < len(b):
+                t, rem = b[pos], len(b) - pos
+                if t == 0:
+                    out.append("Pad0"); pos += 1; continue
+                ln = b[pos + 1] + 2 if rem >= 2 else 0
+                ok = (rem >= 4 and ln == 4) if t == 5 else (rem >= 2 and ln <= rem)
+                if not ok:
+                    stop = 3
+                    break
+                out.append("Padn" if t == 1 else "RouterAlert" if t == 5 else "Generic")
+                pos += ln
+            if stop == 3:
+                break
+        nh, c = f[c], c + hl
+    return out, stop, hdrs
+
+
+def test_ip6_options_model_on_fuzz():
+    hb = gen.make_batch(12, 6000, seed=21)
+    r = oracle.parse_batch(hb.frames, hb.n, flags=FLAGS6, offsets=hb.offsets)
+    o = oracle.options_batch(hb.frames, hb.n, r, offsets=hb.offsets)
+    v = ip6_opts_view(o)
+    stops = set()
+    for i in np.nonzero(is_ip6(r) & ~np.isin(r["status"], [14, 15]))[0]:
+        f = hb.frames[int(hb.offsets[i]):int(hb.offsets[i + 1])].tobytes()
+        kinds, stop, hdrs = model_ip6_opts(f, int(r[i]["l3_off"]), int(r[i]["l4_off"]))
+        assert trace_kinds(o[i]["ip_trace"], o[i]["ip_count"], IP6_OPT_KINDS) == kinds[:16], i
+        assert int(o[i]["ip_count"]) == len(kinds) and int(v[i]["stop"]) == stop, i
+        assert int(v[i]["n_hdrs"]) == hdrs, i
+        stops.add(stop)
+    assert stops == {0, 1, 3}
