@@ -534,6 +534,11 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         barrier(world)
         # the per-rank counters, kept to check the product reduce against torch's own
         local = flow["counters"].clone() if world > 1 else None
+        # one untimed reduce of a zero buffer first: the communicator's creation (own: rank
+        # 0's id broadcast + ncclCommInitRank) and RCCL's first-collective connection setup
+        # are paid once per job, not by the reduce the line reports
+        warm = torch.zeros_like(flow["counters"])
+        rdist.reduce_counters(warm, n_buckets=nb, via=args.reduce_comm)
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
