@@ -173,11 +173,15 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 #ifndef RPKT_LAY_COOP_FILL
 #define RPKT_LAY_COOP_FILL 0     // 1: ... and the new frames' windows loaded cooperatively
 #endif
+#ifndef RPKT_LAY_HALF
+#define RPKT_LAY_HALF 0          // 1: refills fetch the slot's first half, the rest on demand
+#endif
 #ifndef RPKT_LAY_STAGE_MIN
 #define RPKT_LAY_STAGE_MIN 16    // ... when at least this many walks of the wave end together
 #endif
 
 constexpr int kLayChunks = RPKT_LAY_CHUNKS;    // 128 B slot from a 16-B boundary
+constexpr int kLayFill = RPKT_LAY_HALF ? kLayChunks / 2 : kLayChunks;   // chunks per refill
 constexpr int kLaySlot = 16 * kLayChunks + 4;  // 33 dwords: conflict-free lanes
 static_assert((kLaySlot / 4) % 2 == 1, "odd dword stride");
 struct LayScratch {
@@ -213,6 +217,7 @@ struct LayerWin {
         return (v << (ob & 7u)) >> (32u - bits);
     }
     __device__ __forceinline__ void refill(uint32_t s);
+    __device__ __forceinline__ void refill_hi();
 };
 
 // Rare paths of the walk, kept out of line so the loop's hot path stays compact in the
@@ -222,25 +227,29 @@ __device__ __attribute__((noinline)) u32x4 lay_edge16(__amdgpu_buffer_rsrc_t rs,
                                                       uint32_t fb) {
     return load16(rs, a, fb);
 }
-// The slot takes the 128 buffer bytes from the 16-B boundary at or below frame byte s
-// (bytes past the buffer read as 0, as gbyte's; at most one chunk straddles its end).
-__device__ __forceinline__ void LayerWin::refill(uint32_t s) {
-    const uint32_t a = (off + s) & ~15u;
-    u32x4 d[kLayChunks];
+// The slot holds buffer bytes from a 16-B boundary a (frame byte -bias): refill(s) loads
+// its first kLayFill chunks from the boundary at or below frame byte s, refill_hi() the
+// rest from a + 16 kLayFill (RPKT_LAY_HALF: a refill fetches the 64 B most walks stay in,
+// and only a lane whose next header crosses them fetches the second half).  Bytes past
+// the buffer read as 0, as gbyte's; at most one chunk straddles its end.
+template <int K0, int K1>
+__device__ __forceinline__ void lay_load(uint8_t* base, __amdgpu_buffer_rsrc_t rs, uint32_t a,
+                                         uint32_t fb) {
+    u32x4 d[K1 - K0];
 #pragma unroll
-    for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, a + 16u * k);
+    for (int k = K0; k < K1; ++k) d[k - K0] = load16_fast(rs, a + 16u * k);
     uint32_t* w = reinterpret_cast<uint32_t*>(base);
 #pragma unroll
-    for (int k = 0; k < kLayChunks; ++k) {
-        w[4 * k] = d[k].x;
-        w[4 * k + 1] = d[k].y;
-        w[4 * k + 2] = d[k].z;
-        w[4 * k + 3] = d[k].w;
+    for (int k = K0; k < K1; ++k) {
+        w[4 * k] = d[k - K0].x;
+        w[4 * k + 1] = d[k - K0].y;
+        w[4 * k + 2] = d[k - K0].z;
+        w[4 * k + 3] = d[k - K0].w;
     }
     // only the chunk holding the buffer's last byte can straddle its end (chunk
     // (fb - a) / 16, when fb is not on a 16-B boundary): one test, not one per chunk
     const uint32_t rel = fb - a;
-    if (__builtin_expect(fb > a && (rel & 15u) != 0 && rel < 16u * kLayChunks, 0)) {
+    if (__builtin_expect(fb > a && (rel & 15u) != 0 && rel >= 16u * K0 && rel < 16u * K1, 0)) {
         const uint32_t k = rel >> 4;
         const u32x4 v = lay_edge16(rs, a + 16u * k, fb);
         w[4 * k] = v.x;
@@ -248,8 +257,18 @@ __device__ __forceinline__ void LayerWin::refill(uint32_t s) {
         w[4 * k + 2] = v.z;
         w[4 * k + 3] = v.w;
     }
+}
+__device__ __forceinline__ void LayerWin::refill(uint32_t s) {
+    const uint32_t a = (off + s) & ~15u;
+    lay_load<0, kLayFill>(base, rs, a, fb);
     bias = off - a;
-    avail = a + 16u * kLayChunks - off;
+    avail = a + 16u * kLayFill - off;
+}
+__device__ __forceinline__ void LayerWin::refill_hi() {
+    if constexpr (kLayFill < kLayChunks) {
+        lay_load<kLayFill, kLayChunks>(base, rs, off - bias, fb);
+        avail = 16u * kLayChunks - bias;
+    }
 }
 __device__ __attribute__((noinline)) uint32_t lay_far_field(uint8_t* base, uint32_t bias,
                                                             uint32_t avail, uint32_t off,
@@ -270,7 +289,12 @@ struct LayHdr {
 // (the caller then never uses it)
 __device__ __forceinline__ LayHdr lay_hdr(LayerWin& Wn, uint32_t s, bool fill) {
     const bool out = s + 20u > Wn.avail;
-    if (__builtin_expect(out && fill, 0)) Wn.refill(s);
+    if (__builtin_expect(out && fill, 0)) {
+        // the header still starts in the slot's span and ends in its unfetched half:
+        // fetch that half; else the slot moves to the header
+        if (kLayFill < kLayChunks && s + 20u <= 16u * kLayChunks - Wn.bias) Wn.refill_hi();
+        else Wn.refill(s);
+    }
     const uint32_t y = out && !fill ? 0u : s + Wn.bias, a = y & ~3u;
     uint32_t R[6];
 #pragma unroll
@@ -678,13 +702,13 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 #pragma unroll
     for (int k = 0; k < FR; ++k) fr[k] = spans.get(p0 + lane + kWave * k);
     {
-        u32x4 d[kLayChunks];
-        uint32_t addr[kLayChunks];
+        u32x4 d[kLayFill];
+        uint32_t addr[kLayFill];
         uint32_t fix = 0;
 #pragma unroll
-        for (int k = 0; k < kLayChunks; ++k) {
+        for (int k = 0; k < kLayFill; ++k) {
             const int c = k * kWave + lane;
-            const int q = c / kLayChunks, j = c % kLayChunks;
+            const int q = c / kLayFill, j = c % kLayFill;
             const uint32_t qo = (uint32_t)__shfl((int)fr[0].off, q, kWave);
             const uint32_t ql = (uint32_t)__shfl((int)fr[0].len, q, kWave);
             const uint32_t a = (qo & ~15u) + 16u * j;
@@ -692,14 +716,14 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             fix |= (uint32_t)straddles(addr[k], fb) << k;
         }
 #pragma unroll
-        for (int k = 0; k < kLayChunks; ++k) d[k] = load16_fast(rs, addr[k]);
+        for (int k = 0; k < kLayFill; ++k) d[k] = load16_fast(rs, addr[k]);
 #pragma unroll
-        for (int k = 0; k < kLayChunks; ++k) {
+        for (int k = 0; k < kLayFill; ++k) {
             const int c = k * kWave + lane;
             u32x4 v = d[k];
             if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kLayChunks) * kLaySlot +
-                                                              (c % kLayChunks) * 16]);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&W.win[(c / kLayFill) * kLaySlot +
+                                                              (c % kLayFill) * 16]);
             dst[0] = v.x;
             dst[1] = v.y;
             dst[2] = v.z;
@@ -708,7 +732,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
     wave_sync();
 
-    LayerWin Wn{&W.win[lane * kLaySlot], fr[0].off & 15u, (uint32_t)(kLayChunks * 16) - (fr[0].off & 15u),
+    LayerWin Wn{&W.win[lane * kLaySlot], fr[0].off & 15u, (uint32_t)(kLayFill * 16) - (fr[0].off & 15u),
                 fr[0].off, fb, rs};
     uint32_t o[16];
 #pragma unroll
@@ -895,7 +919,7 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                 if (active) {
                     if constexpr ((ABL & 1) != 0) {
                         Wn.bias = f.off & 15u;
-                        Wn.avail = (uint32_t)(kLayChunks * 16) - Wn.bias;
+                        Wn.avail = (uint32_t)(kLayFill * 16) - Wn.bias;
                     } else if (filled) {
                         Wn.bias = f.off & 15u;
                         Wn.avail = (uint32_t)(kLayChunks * 16) - Wn.bias;

@@ -10,7 +10,7 @@ import pytest
 from oracle import oracle
 from rpkt_amd import engine, gen
 from rpkt_amd.records import (F_FLOW_EV, F_IPV6, STATUS, as_opts, as_records, as_records16,
-                              is_ip6, project16)
+                              ip6_opts_view, is_ip6, project16)
 
 from test_gpu_parity import assert_same, assert_same16, host_batch
 
@@ -216,11 +216,15 @@ def _opts_check(db, hb, flags):
 
 @pytest.mark.parametrize("cfg,n", [(11, 200000), (12, None)])
 def test_option_walks_over_ip6(torch, cfg, n):
-    """TcpOptionsIter runs over IPv6/TCP frames too; Ipv4OptionsIter never over IPv6."""
+    """TcpOptionsIter runs over IPv6/TCP frames too; Ipv4OptionsIter never over IPv6 (its
+    bytes of an IPv6 frame's row are the Ipv6OptionsIter view: stop NONE without an
+    option header, END or MALFORMED after walking one)."""
     hb = gen.make_batch(cfg, n)
     want, o = _opts_check(engine.DeviceBatch.from_host(hb), hb, F6)
     v6 = is_ip6(o)
-    assert (want["ip_stop"][v6] == 0).all()
+    walked = ip6_opts_view(want)["n_hdrs"] != 0
+    assert set(np.unique(want["ip_stop"][v6 & ~walked])) <= {0}
+    assert set(np.unique(want["ip_stop"][v6 & walked])) <= {1, 3}
     tcp6 = v6 & (o["status"] == 0) & (o["ip_protocol"] == 6)
     assert tcp6.any() and (want["tcp_stop"][tcp6] != 0).all()
 

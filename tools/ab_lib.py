@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7]
+Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7]
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--n", type=int, default=0, help="frames per batch (default: the config's)")
+    ap.add_argument("--sides", default="AB",
+                    help="sides to launch (a rocprofv3 --pmc pass of one build: A or B)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches per side (default: 8 at 64 B, as bench.py)")
     args, extra = ap.parse_known_args()
@@ -188,7 +190,7 @@ def main():
         outs[name] = out
     times = {"A": [], "B": []}
     for rnd in range(args.rounds + 1):
-        for name in ("A", "B"):
+        for name in args.sides:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for k in range(args.launches):
@@ -198,11 +200,11 @@ def main():
             torch.cuda.synchronize()
             if rnd:
                 times[name].append(e0.elapsed_time(e1) / args.launches * 1e3)
-    same = all(outs[k].cpu().numpy().tobytes() == outs["B" + k[1:]].cpu().numpy().tobytes()
-               for k in outs if k.startswith("A"))
+    same = args.sides == "AB" and all(
+        outs[k].cpu().numpy().tobytes() == outs["B" + k[1:]].cpu().numpy().tobytes()
+        for k in outs if k.startswith("A"))
     print(json.dumps({"leg": args.leg, "n": hb.n, "rotate": R, "identical": same,
-                      "A_us": round(float(np.median(times["A"])), 2),
-                      "B_us": round(float(np.median(times["B"])), 2)}))
+                      **{s + "_us": round(float(np.median(times[s])), 2) for s in args.sides}}))
 
 
 if __name__ == "__main__":
