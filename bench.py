@@ -537,8 +537,8 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         # one untimed reduce of a zero buffer first: the communicator's creation (own: rank
         # 0's id broadcast + ncclCommInitRank) and RCCL's first-collective connection setup
         # are paid once per job, not by the reduce the line reports
-        warm = torch.zeros_like(flow["counters"])
-        rdist.reduce_counters(warm, n_buckets=nb, via=args.reduce_comm)
+        zeros = torch.zeros_like(flow["counters"])
+        rdist.reduce_counters(zeros, n_buckets=nb, via=args.reduce_comm)
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
