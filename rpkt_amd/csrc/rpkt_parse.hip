@@ -216,8 +216,28 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     const int wid = threadIdx.x / kWave;
     const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
     if (p0 >= n) return;                                          // wave-uniform exit
+#ifdef RPKT_ABLATE
+    // V == 50 (tools/launch_stamps.py): the wave's start and end on the 100-MHz clock all
+    // CUs share, after its stores are acknowledged, and where it ran; flow_ev is the stamp
+    // buffer (4 u64 per wave) and the flags carry no RPKT_F_FLOW_EV
+    uint64_t t0 = 0;
+    if constexpr (V == 50) t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     parse_tile<L4, V, C16, OPTS>(scratch[wid], opt_rules, frames, frames_bytes, offsets, stride,
                                  frame_len, n, flags, recs, flow_ev, n_buckets, opts, p0, lane);
+#ifdef RPKT_ABLATE
+    if constexpr (V == 50) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);    // XCC_ID
+        if (lane == 0) {
+            u32x4* st = reinterpret_cast<u32x4*>(flow_ev) + 2u * (p0 / kWave);
+            st[0] = u32x4{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1, (uint32_t)(t1 >> 32)};
+            st[1] = u32x4{hw, xcc, 0u, 0u};
+        }
+    }
+#endif
 }
 
 // A receive ring's slots in one launch (rpkt_gpu_parse_ring): wave t takes tile t of the
@@ -1297,6 +1317,20 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
         default: return RPKT_E_INVAL;
     }
 #undef RPKT_V
+}
+
+// The parse with per-wave clock stamps (variant 50, 32 B per wave of the grid in
+// stamps_dev), for tools/launch_stamps.py: where a launch's fixed cost goes.
+int rpkt_gpu_debug_stamps(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs,
+                          void* stamps_dev, void* stream) {
+    if (!b || !recs || !stamps_dev || b->n == 0 || (flags & RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch((flags & RPKT_F_L4_SUM) ? parse_kernel<true, 50> : parse_kernel<false, 50>,
+                  dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags & kParseFlags,
+                  recs, (uint64_t*)stamps_dev, 0u, (rpkt_opts_t*)nullptr);
 }
 
 #endif  // RPKT_ABLATE
