@@ -197,14 +197,15 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     }
 }
 
-template <bool L4, int V, bool C16 = false, bool OPTS = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)    // 4 waves/SIMD: <= 128 VGPRs
+// WPB: waves per block (a block's slot on its CU is freed when its last wave ends)
+template <bool L4, int V, bool C16 = false, bool OPTS = false, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * WPB, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                   uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ recs,
                   uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
                   rpkt_opts_t* __restrict__ opts) {
-    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[WPB];
     // the option-type rules of both iterators (OPTS; 4 + 4 x 9744 + 512 B: still four
     // blocks per CU)
     __shared__ uint8_t opt_rules[OPTS ? 512 : 4];
@@ -214,7 +215,7 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     }
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
-    const uint32_t p0 = (blockIdx.x * kWavesPerBlock + wid) * kWave;
+    const uint32_t p0 = (blockIdx.x * WPB + wid) * kWave;
     if (p0 >= n) return;                                          // wave-uniform exit
 #ifdef RPKT_ABLATE
     // V == 50 (tools/launch_stamps.py): the wave's start and end on the 100-MHz clock all
@@ -1321,16 +1322,32 @@ int rpkt_gpu_debug_variant(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* re
 
 // The parse with per-wave clock stamps (variant 50, 32 B per wave of the grid in
 // stamps_dev), for tools/launch_stamps.py: where a launch's fixed cost goes.
-int rpkt_gpu_debug_stamps(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs,
-                          void* stamps_dev, void* stream) {
-    if (!b || !recs || !stamps_dev || b->n == 0 || (flags & RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+// wpb: waves per block, 1, 2 or 4 (the product's); stamps_dev may be null (variant 0:
+// the product kernel at that block size)
+extern "C++" template <int WPB>
+int launch_stamps(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs, void* stamps_dev,
+                  hipStream_t st) {
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t per_block = kWave * WPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch((flags & RPKT_F_L4_SUM) ? parse_kernel<true, 50> : parse_kernel<false, 50>,
-                  dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
-                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags & kParseFlags,
-                  recs, (uint64_t*)stamps_dev, 0u, (rpkt_opts_t*)nullptr);
+    const bool l4 = (flags & RPKT_F_L4_SUM) != 0;
+    auto k = stamps_dev ? (l4 ? parse_kernel<true, 50, false, false, WPB>
+                              : parse_kernel<false, 50, false, false, WPB>)
+                        : (l4 ? parse_kernel<true, 0, false, false, WPB>
+                              : parse_kernel<false, 0, false, false, WPB>);
+    return launch(k, dim3(grid), dim3(per_block), 0, st, b->frames_dev, (uint32_t)b->frames_bytes,
+                  b->offsets_dev, b->stride, flen, b->n, flags & kParseFlags, recs,
+                  (uint64_t*)stamps_dev, 0u, (rpkt_opts_t*)nullptr);
+}
+int rpkt_gpu_debug_stamps(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs,
+                          void* stamps_dev, int wpb, void* stream) {
+    if (!b || !recs || b->n == 0 || (flags & RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    switch (wpb) {
+        case 1: return launch_stamps<1>(b, flags, recs, stamps_dev, (hipStream_t)stream);
+        case 2: return launch_stamps<2>(b, flags, recs, stamps_dev, (hipStream_t)stream);
+        case 4: return launch_stamps<4>(b, flags, recs, stamps_dev, (hipStream_t)stream);
+        default: return RPKT_E_INVAL;
+    }
 }
 
 #endif  // RPKT_ABLATE

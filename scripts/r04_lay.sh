@@ -9,15 +9,17 @@ O=$R/gpurun_out/r04_lay
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 AB="$R/tools/ab_lib.py"
-for B in ${BSIDES:-half}; do
-  for leg in layers9 layers2 layers5; do
+BSIDES=${BSIDES:-half}
+for B in $BSIDES; do
+  for leg in ${LEGS-layers9 layers2 layers5}; do
     timeout -k 10 300 python3 -u "$AB" "$R/ab/$B/librpkt_gpu.so" --leg $leg --rounds 7 --launches 20 \
         >> "$O/ab_$B.jsonl" 2>> "$O/ab_$B.log" || exit 1
   done
 done
-for side in A ${BSIDES:-half}; do
+B1=${BSIDES%% *}
+for side in A $BSIDES; do
   lib="$R/ab/${side}/librpkt_gpu.so"; s=B
-  if [ "$side" = A ]; then lib="$R/ab/${BSIDES%% *}/librpkt_gpu.so"; s=A; fi
+  if [ "$side" = A ]; then lib="$R/ab/$B1/librpkt_gpu.so"; s=A; fi
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $c -T --output-format csv -d "$O/pmc_${side}_$c" -o p \
         -- python3 "$AB" "$lib" --leg layers9 --sides $s --rounds 1 --launches 10 \

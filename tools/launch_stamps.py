@@ -9,8 +9,11 @@ and reports per launch, in microseconds from the launch's first wave start:
   * the drain: when the k-th percentile of waves ended, the last end,
   * the gap between one launch's last wave end and the next one's first wave start,
   * the mean wave duration, waves in flight at the plateau, and per-XCD last ends.
+Each block size in --wpb (waves per block; the product's is 4) is measured, and the
+unstamped kernel at that block size is timed with HIP events over the same sequence.
 Usage: python tools/launch_stamps.py [--n 1048576] [--launches 40] [--flags 1] [--config 2]
-Prints one JSON line.
+                                     [--wpb 4,2,1]
+Prints one JSON line per block size.
 """
 import argparse
 import ctypes
@@ -34,11 +37,12 @@ def main():
     ap.add_argument("--launches", type=int, default=40)
     ap.add_argument("--flags", type=int, default=1)
     ap.add_argument("--rotate", type=int, default=8)
+    ap.add_argument("--wpb", default="4,2,1")
     args = ap.parse_args()
     L = engine.ablate_lib()
     P = ctypes.POINTER(engine.Batch)
     L.rpkt_gpu_debug_stamps.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p]
+                                        ctypes.c_int, ctypes.c_void_p]
     R = args.rotate
     hbs = [gen.make_batch(args.config, args.n, seed=gen.DEFAULT_SEED[args.config] + 104729 * r)
            for r in range(R)]
@@ -51,28 +55,34 @@ def main():
     st = torch.cuda.current_stream()
     sp = ctypes.c_void_p(st.cuda_stream)
 
-    def run(k):
+    def run(k, wpb, stamped=True):
         rc = L.rpkt_gpu_debug_stamps(ctypes.byref(descs[k % R]), args.flags, recs[k % R].data_ptr(),
-                                     stamps[k].data_ptr(), sp)
+                                     stamps[k].data_ptr() if stamped else None, wpb, sp)
         assert rc == 0, rc
 
-    for k in range(K):                               # warm: clocks ramp
-        run(k)
-    torch.cuda.synchronize()
-    # product kernel, same sequence, HIP events (what the bench reports)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for k in range(K):
-        engine.parse_batch(dbs[k % R], args.flags, recs=recs[k % R])
-    e1.record(st)
-    torch.cuda.synchronize()
-    product_us = e0.elapsed_time(e1) * 1e3 / K
-    e0.record(st)
-    for k in range(K):
-        run(k)
-    e1.record(st)
-    torch.cuda.synchronize()
-    stamped_us = e0.elapsed_time(e1) * 1e3 / K
+    def timed(wpb, stamped):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for k in range(K):
+            run(k, wpb, stamped)
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / K
+
+    want = engine.parse_batch(dbs[0], args.flags).cpu()
+    for wpb in [int(x) for x in args.wpb.split(",")]:
+        recs[0].zero_()
+        for k in range(K):                           # warm: clocks ramp
+            run(k, wpb)
+        torch.cuda.synchronize()
+        assert torch.equal(recs[0].cpu(), want), "records differ at wpb %d" % wpb
+        plain = [timed(wpb, False) for _ in range(3)]
+        stamped_us = timed(wpb, True)
+        report(args, stamps, K, wpb, float(np.median(plain)), stamped_us)
+
+
+def report(args, stamps, K, wpb, product_us, stamped_us):
+    waves = stamps.shape[1]
     s = stamps.cpu().numpy()
     t0 = s[:, :, 0].astype(np.int64)
     t1 = s[:, :, 1].astype(np.int64)
@@ -95,13 +105,14 @@ def main():
         inflight.append(started - ended)
     inflight = np.median(np.array(inflight), axis=0)
     plateau = float(np.percentile(inflight, 75))
+    mid = float(inflight[10:80].mean())             # mean waves in flight, 10-80 % of the span
     cu = (hw >> 8) & 0xf
     se = (hw >> 13) & 0x7
     last_end_xcd = {int(x): round(float(np.median([rel1[k][xcc[k] == x].max() for k in range(K)])), 2)
                     for x in np.unique(xcc)}
     out = {
-        "config": args.config, "n": args.n, "waves": waves, "launches": K,
-        "product_us_per_launch": round(product_us, 2),
+        "config": args.config, "n": args.n, "waves": waves, "launches": K, "wpb": wpb,
+        "kernel_us_per_launch": round(product_us, 2),
         "stamped_us_per_launch": round(stamped_us, 2),
         "span_first_start_to_last_end_us": round(float(np.median(span)), 2),
         "gap_last_end_to_next_first_start_us": round(float(np.median(gaps)), 2),
@@ -110,6 +121,7 @@ def main():
         "wave_us_mean": round(float(dur.mean()), 3),
         "wave_us_pct": {p: round(float(np.percentile(dur, p)), 3) for p in (10, 50, 90, 99)},
         "inflight_plateau": plateau,
+        "inflight_mean_10_80": round(mid, 1),
         "inflight_profile": [int(x) for x in inflight[::5]],
         "xcds": int(len(np.unique(xcc))),
         "cus_seen": int(len(np.unique(xcc * 1024 + se * 16 + cu))),
