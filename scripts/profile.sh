@@ -15,4 +15,9 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT" -o
     -- python3 "$R/bench.py" "${ARGS[@]}" > "$OUT/fetch_bench.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT" -o write \
     -- python3 "$R/bench.py" "${ARGS[@]}" > "$OUT/write_bench.log" 2>&1
+# read requests by size (TCC_EA0_RDREQ_{32B,64B,128B} + all: the 4 TCC slots): the exact
+# read bytes, which calibrate FETCH_SIZE's x2 for access shapes other than streaming
+timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+    TCC_EA0_RDREQ_sum -T --output-format csv -d "$OUT" -o rdreq \
+    -- python3 "$R/bench.py" "${ARGS[@]}" > "$OUT/rdreq_bench.log" 2>&1
 echo "profile $TAG (config $CFG) done"

@@ -22,6 +22,28 @@ def rows(path):
         return list(csv.DictReader(fh))
 
 
+RDREQ = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_128B_sum": 128}
+
+
+def rdreq(prof, kname):
+    """The read requests by size of the optional `rdreq` pass (scripts/profile.sh), per
+    launch of kernel kname (warm-up launches skipped): {counter: requests, "read_bytes":
+    32 n32 + 64 n64 + 128 n128, "requests": all}, or None without that pass."""
+    path = os.path.join(prof, "rdreq_counter_collection.csv")
+    if not os.path.exists(path):
+        return None
+    by = {}
+    for r in rows(path):
+        if r["Kernel_Name"].startswith(kname):
+            by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if not by:
+        return None
+    avg = {k: sum(v[5:]) / len(v[5:]) if len(v) > 5 else sum(v) / len(v) for k, v in by.items()}
+    res = {k: avg.get(k, 0.0) for k in list(RDREQ) + ["TCC_EA0_RDREQ_sum"]}
+    res["read_bytes"] = sum(avg.get(k, 0.0) * b for k, b in RDREQ.items())
+    return res
+
+
 def main(prof, cfg, out):
     kname = "parse_chains_kernel" if cfg in (7, 8) else "parse_kernel"
     tr = [r for r in rows(os.path.join(prof, "trace_kernel_trace.csv"))
@@ -53,6 +75,11 @@ def main(prof, cfg, out):
         "traffic_bytes_per_launch": fetch_kib * 1024 * 2 + write_kib * 1024,
         "kernel_stats": stats,
     }
+    rq = rdreq(prof, kname)
+    if rq:
+        res["rdreq"] = rq
+        res["read_bytes_by_request_size"] = rq["read_bytes"]
+        res["fetch_x2_over_by_size"] = fetch_kib * 2048 / rq["read_bytes"] if rq["read_bytes"] else None
     os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
@@ -119,6 +146,10 @@ def main_tx(prof, out, only=None):
         legs[leg] = {"kernel": kname, "fetch_size_kib": f, "write_size_kib": w,
                      "hbm_read_bytes_corrected": f * 1024 * 2, "hbm_write_bytes": w * 1024,
                      "traffic_bytes_per_launch": f * 1024 * 2 + w * 1024, "engine_build": build}
+        rq = rdreq(prof, kname)
+        if rq:
+            legs[leg].update(rdreq=rq, read_bytes_by_request_size=rq["read_bytes"],
+                             fetch_x2_over_by_size=f * 2048 / rq["read_bytes"] if rq["read_bytes"] else None)
     res = {"engine_build": build, "legs": legs,
            "kernel_stats": rows(os.path.join(prof, "trace_kernel_stats.csv"))}
     # keep the stats of the single-leg profiles whose legs were kept
