@@ -783,6 +783,24 @@ def copy_ceiling(dbs, recs, steps):
 FORBID_IPS = ["192.168.5.%d" % k for k in range(3, 11)]    # loopback_rx.rs:42-51
 
 
+def line_floor(starts, ends, line=128):
+    """Bytes of the distinct `line`-byte lines of the frame buffer that hold any byte of
+    the ranges [starts, ends): the least a kernel reading exactly those bytes fetches,
+    since every read request the memory side sends on gfx950 is a whole 128-B line
+    (TCC_EA0_RDREQ_128B = all requests, profiles/r04_rdreq/)."""
+    starts, ends = np.asarray(starts, np.int64), np.asarray(ends, np.int64)
+    m = ends > starts
+    a, b = starts[m] // line, (ends[m] - 1) // line
+    if a.size == 0:
+        return 0
+    o = np.argsort(a, kind="stable")
+    a, b = a[o], b[o]
+    new = np.ones(a.size, bool)
+    new[1:] = a[1:] > np.maximum.accumulate(b)[:-1]
+    idx = np.flatnonzero(new)
+    return int((np.maximum.reduceat(b, idx) - a[idx] + 1).sum()) * line
+
+
 def ip_u32(s):
     a, b, c, d = (int(x) for x in s.split("."))
     return (a << 24) | (b << 16) | (c << 8) | d
@@ -883,9 +901,14 @@ def run_tx(cfg, mode, args, rank, world):
     fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
     if mode == "build":
         alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
-    elif mode == "layers":                     # header bytes walked + 64 B out per frame
+    floor = None                               # the 128-B line floor of the reads + writes
+    fo = hbs[0].offsets[:-1].astype(np.int64) if hbs[0].offsets is not None else \
+        np.arange(hbs[0].n, dtype=np.int64) * hbs[0].stride
+    if mode == "layers":                       # header bytes walked + 64 B out per frame
         lo = outs[0].cpu().numpy().view(LAYERS_DTYPE)
-        alg = int(np.minimum(lo["payload_off"].astype(np.int64), lens).sum()) + hbs[0].n * 64
+        walked = np.minimum(lo["payload_off"].astype(np.int64), lens)
+        alg = int(walked.sum()) + hbs[0].n * 64
+        floor = line_floor(fo, fo + walked) + hbs[0].n * 64
     elif mode == "fields":                     # layer records + field bytes read, values written
         pm = pres[0].cpu().numpy().view(np.uint32)
         nbytes = [(int(q["bit_off"]) + int(q["bits"]) - 1) // 8 - int(q["bit_off"]) // 8 + 1
@@ -895,9 +918,14 @@ def run_tx(cfg, mode, args, rank, world):
     elif mode in ("opts", "optsc"):            # records + option slices read, 64 B written
         ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
-        slices = np.where(ip_parsed, r["l4_off"].astype(np.int64) - r["l3_off"] - 20, 0) + \
-            np.where(tcp, r["payload_off"].astype(np.int64) - r["l4_off"] - 20, 0)
-        alg = hbs[0].n * ((REC16_BYTES if mode == "optsc" else REC_BYTES) + 64) + int(slices.sum())
+        l3, l4 = r["l3_off"].astype(np.int64), r["l4_off"].astype(np.int64)
+        po = r["payload_off"].astype(np.int64)
+        slices = np.where(ip_parsed, l4 - l3 - 20, 0) + np.where(tcp, po - l4 - 20, 0)
+        fixed_io = hbs[0].n * ((REC16_BYTES if mode == "optsc" else REC_BYTES) + 64)
+        alg = fixed_io + int(slices.sum())
+        floor = fixed_io + line_floor(
+            np.concatenate([np.where(ip_parsed, fo + l3 + 20, 0), np.where(tcp, fo + l4 + 20, 0)]),
+            np.concatenate([np.where(ip_parsed, fo + l4, 0), np.where(tcp, fo + po, 0)]))
     else:
         kept = outs[0].cpu().numpy().astype(bool)
         alg = int(lens.sum()) + hbs[0].n + int(kept.sum()) * 42
@@ -908,7 +936,9 @@ def run_tx(cfg, mode, args, rank, world):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "alg_bytes_per_launch": alg, "traffic": traffic,
-                         "traffic_source": tsrc},
+                         "traffic_source": tsrc, "line_floor_bytes": floor,
+                         "traffic_over_floor": round(traffic / floor, 4)
+                         if traffic and floor else None},
             "what": ("build: Udp|Tcp/Ipv4/Ether prepend_header + setters, IPv4 + L4 checksum "
                      "fill" if mode == "build" else
                      "options: Ipv4OptionsIter + TcpOptionsIter walks of a parsed batch"

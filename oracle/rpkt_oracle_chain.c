@@ -33,6 +33,8 @@ int oracle_from_slice_with_tail_byte(const uint8_t* data, size_t len, uint32_t* 
                                      int tail_in);
 uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
                                  uint16_t length);
+uint16_t oracle_pseudo_header_v6(const uint8_t* src16, const uint8_t* dst16, uint8_t proto,
+                                 uint32_t length);
 uint64_t oracle_flow_event(const rpkt_rec_t* r, uint32_t n_buckets);
 
 /* ------------------------------------------------------------------------- */
@@ -161,6 +163,161 @@ static uint32_t be32(const uint8_t* p) {
 /* The decode chain over a Pbuf                                               */
 /* ------------------------------------------------------------------------- */
 
+/* Udp::parse / Tcp::parse over the Pbuf the IP layer's payload() returned (header
+ * sizes against chunk().len(), the UDP length against remaining()), getters, the L4
+ * sum with the pseudo header of the IP version, payload().  Shared by both chains. */
+static void parse_pbuf_l4(pbuf_t* bufp, uint8_t proto, const uint8_t* src, const uint8_t* dst,
+                          int v6, uint32_t flags, rpkt_rec_t* rec) {
+    pbuf_t buf = *bufp;
+    if (proto == 17) {
+        /* Udp::parse, udp/generated.rs:31-42 */
+        if (buf.chunk_len < 8) { rec->status = RPKT_S_UDP_SHORT; return; }
+        const uint8_t* u = pbuf_chunk(&buf);
+        uint64_t ulen = be16(u + 4);
+        if (ulen < 8 || ulen > pbuf_remaining(&buf)) { rec->status = RPKT_S_UDP_BAD_LEN; return; }
+        rec->src_port = be16(u);
+        rec->dst_port = be16(u + 2);
+        rec->l4_word6 = (uint16_t)ulen;
+        rec->l4_checksum = be16(u + 6);
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {v6 ? oracle_pseudo_header_v6(src, dst, 17, (uint32_t)ulen)
+                                    : oracle_pseudo_header_v4(src, dst, 17, (uint16_t)ulen),
+                                 pbuf_from_buf(buf, ulen)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        /* Udp::payload, udp/generated.rs:66-76 */
+        uint64_t ts = pbuf_remaining(&buf) - ulen;
+        if (ts > 0) pbuf_trim_off(&buf, ts);
+        pbuf_advance(&buf, 8);
+        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
+        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+        rec->status = RPKT_S_OK;
+    } else if (proto == 6) {
+        /* Tcp::parse, tcp/generated.rs:34-45 */
+        uint64_t cl = buf.chunk_len;
+        if (cl < 20) { rec->status = RPKT_S_TCP_SHORT; return; }
+        const uint8_t* t = pbuf_chunk(&buf);
+        uint64_t hl = (uint64_t)(t[12] >> 4) * 4;
+        if (hl < 20 || hl > cl) { rec->status = RPKT_S_TCP_BAD_DOFF; return; }
+        rec->src_port = be16(t);
+        rec->dst_port = be16(t + 2);
+        rec->tcp_seq = be32(t + 4);
+        rec->tcp_ack = be32(t + 8);
+        rec->l4_word6 = be16(t + 12);
+        rec->tcp_window = be16(t + 14);
+        rec->l4_checksum = be16(t + 16);
+        rec->tcp_urgent = be16(t + 18);
+        uint64_t l4len = pbuf_remaining(&buf);        /* TCP length comes from the IP layer */
+        if (flags & RPKT_F_L4_SUM) {
+            uint16_t parts[2] = {v6 ? oracle_pseudo_header_v6(src, dst, 6, (uint32_t)l4len)
+                                    : oracle_pseudo_header_v4(src, dst, 6, (uint16_t)l4len),
+                                 pbuf_from_buf(buf, l4len)};
+            rec->l4_sum = oracle_combine(parts, 2);
+        }
+        pbuf_advance(&buf, hl);                       /* Tcp::payload :125-131 */
+        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
+        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+        rec->status = RPKT_S_OK;
+    } else {
+        rec->status = RPKT_S_L4_OTHER;
+    }
+}
+
+static uint32_t fold_be32x4(const uint8_t* a) {
+    return be32(a) ^ be32(a + 4) ^ be32(a + 8) ^ be32(a + 12);
+}
+
+/* The IPv6 chain over a Pbuf (RPKT_F_IPV6): oracle_parse_ip6 (rpkt_oracle.c) with every
+ * header size tested against chunk().len() and the payload length against
+ * remaining(): Ipv6::parse ipv6/generated.rs:40-51, payload :83-92, then each
+ * extension header's generated parse (DestOptions :241-252, HopByHopOption :384-395,
+ * RoutingHeader :528-539, FragmentHeader :696-703, AuthenticationHeader :850-861) and
+ * payload() = advance(header_len). */
+static void parse_pbuf_ip6(pbuf_t* bufp, uint32_t flags, rpkt_rec_t* rec) {
+    pbuf_t buf = *bufp;
+    rec->l3_off = (uint16_t)pbuf_cursor(&buf);
+    if (buf.chunk_len < 40) { rec->status = RPKT_S_IP6_SHORT; return; }       /* :42 */
+    const uint8_t* ip = pbuf_chunk(&buf);            /* the header lies inside the chunk */
+    uint64_t payload_len = be16(ip + 4);
+    if (payload_len + 40 > pbuf_remaining(&buf)) { rec->status = RPKT_S_IP6_BAD_LEN; return; }
+    uint8_t* blk = (uint8_t*)rec + 24;
+    uint32_t vtcfl = be32(ip);
+    uint16_t pl = (uint16_t)payload_len;
+    uint16_t pdst_off = (uint16_t)(pbuf_cursor(&buf) + 24);
+    uint32_t sf = fold_be32x4(ip + 8), df = fold_be32x4(ip + 24);
+    memcpy(blk + 0, &vtcfl, 4);
+    memcpy(blk + 4, &pl, 2);
+    blk[6] = ip[6];
+    blk[7] = ip[7];
+    memcpy(blk + 12, &sf, 4);
+    memcpy(blk + 16, &df, 4);
+    const uint8_t* pdst = ip + 24;
+
+    /* Ipv6::payload, :83-92 */
+    uint64_t trim_size = pbuf_remaining(&buf) - (40 + payload_len);
+    if (trim_size > 0) pbuf_trim_off(&buf, trim_size);
+    pbuf_advance(&buf, 40);
+
+    uint8_t nh = ip[6];
+    uint8_t n_ext = 0;
+    int stop = 0;
+    for (; n_ext < RPKT_MAX_IP6_EXT; n_ext++) {
+        uint64_t cl = buf.chunk_len;
+        const uint8_t* h = pbuf_chunk(&buf);
+        uint64_t hl;
+        if (nh == 0 || nh == 60) {
+            if (cl < 2) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (uint64_t)h[1] * 8 + 8;
+            if (hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        } else if (nh == 43) {
+            if (cl < 8) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (uint64_t)h[1] * 8 + 8;
+            if (hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+            if (h[3] > 0) {                          /* segments_left: the final address */
+                uint64_t n_addr = (hl - 8) / 16;
+                const uint8_t* q = pdst;
+                if (h[2] == 4 && n_addr >= 1) q = h + 8;
+                else if ((h[2] == 0 || h[2] == 2) && n_addr >= 1) q = h + 8 + 16 * (n_addr - 1);
+                if (q != pdst) {
+                    pdst = q;
+                    pdst_off = (uint16_t)(pbuf_cursor(&buf) + (uint64_t)(q - h));
+                }
+            }
+        } else if (nh == 44) {
+            if (cl < 8) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = 8;
+            uint16_t off = (uint16_t)(be16(h + 2) >> 3);
+            if (off != 0 || (h[3] & 1)) {
+                nh = h[0];
+                pbuf_advance(&buf, hl);
+                n_ext++;
+                stop = RPKT_S_IP6_FRAGMENT;
+                break;
+            }
+        } else if (nh == 51) {
+            if (cl < 12) { stop = RPKT_S_IP6_EXT_SHORT; break; }
+            hl = (uint64_t)h[1] * 4 + 8;
+            if (hl < 12 || hl > cl) { stop = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        } else {
+            break;
+        }
+        nh = h[0];
+        pbuf_advance(&buf, hl);
+    }
+    blk[8] = n_ext;
+    blk[9] = nh;
+    memcpy(blk + 10, &pdst_off, 2);
+    rec->l4_off = (uint16_t)pbuf_cursor(&buf);
+    rec->payload_off = rec->l4_off;
+    rec->payload_len = (uint16_t)pbuf_remaining(&buf);
+    if (stop) { rec->status = (uint8_t)stop; return; }
+    if (nh == 0 || nh == 43 || nh == 44 || nh == 60 || nh == 51) {
+        rec->status = RPKT_S_L4_OTHER;
+        return;
+    }
+    parse_pbuf_l4(&buf, nh, ip + 8, pdst, 1, flags, rec);
+}
+
 /* Same chain and record as oracle_parse_one (rpkt_oracle.c), with every length
  * test taken exactly as the generic views take it: header sizes against
  * chunk().len(), IPv4/UDP totals against remaining(). */
@@ -189,6 +346,7 @@ static void parse_pbuf(mchain_t* m, uint32_t flags, rpkt_rec_t* rec) {
         rec->n_vlan++;
         pbuf_advance(&buf, 4);
     }
+    if (et == 0x86dd && (flags & RPKT_F_IPV6)) { parse_pbuf_ip6(&buf, flags, rec); return; }
     if (et != 0x0800) { rec->status = RPKT_S_NOT_IPV4; return; }
 
     /* Ipv4::parse, ipv4/generated.rs:35-51 */
@@ -224,57 +382,7 @@ static void parse_pbuf(mchain_t* m, uint32_t flags, rpkt_rec_t* rec) {
     rec->payload_off = rec->l4_off;
     rec->payload_len = (uint16_t)pbuf_remaining(&buf);
 
-    uint8_t proto = ip[9];
-    if (proto == 17) {
-        /* Udp::parse, udp/generated.rs:31-42 */
-        if (buf.chunk_len < 8) { rec->status = RPKT_S_UDP_SHORT; return; }
-        const uint8_t* u = pbuf_chunk(&buf);
-        uint64_t ulen = be16(u + 4);
-        if (ulen < 8 || ulen > pbuf_remaining(&buf)) { rec->status = RPKT_S_UDP_BAD_LEN; return; }
-        rec->src_port = be16(u);
-        rec->dst_port = be16(u + 2);
-        rec->l4_word6 = (uint16_t)ulen;
-        rec->l4_checksum = be16(u + 6);
-        if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 17, (uint16_t)ulen),
-                                 pbuf_from_buf(buf, ulen)};
-            rec->l4_sum = oracle_combine(parts, 2);
-        }
-        /* Udp::payload, udp/generated.rs:66-76 */
-        uint64_t ts = pbuf_remaining(&buf) - ulen;
-        if (ts > 0) pbuf_trim_off(&buf, ts);
-        pbuf_advance(&buf, 8);
-        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
-        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
-        rec->status = RPKT_S_OK;
-    } else if (proto == 6) {
-        /* Tcp::parse, tcp/generated.rs:34-45 */
-        uint64_t cl = buf.chunk_len;
-        if (cl < 20) { rec->status = RPKT_S_TCP_SHORT; return; }
-        const uint8_t* t = pbuf_chunk(&buf);
-        uint64_t hl = (uint64_t)(t[12] >> 4) * 4;
-        if (hl < 20 || hl > cl) { rec->status = RPKT_S_TCP_BAD_DOFF; return; }
-        rec->src_port = be16(t);
-        rec->dst_port = be16(t + 2);
-        rec->tcp_seq = be32(t + 4);
-        rec->tcp_ack = be32(t + 8);
-        rec->l4_word6 = be16(t + 12);
-        rec->tcp_window = be16(t + 14);
-        rec->l4_checksum = be16(t + 16);
-        rec->tcp_urgent = be16(t + 18);
-        uint64_t l4len = pbuf_remaining(&buf);        /* TCP length comes from IPv4 */
-        if (flags & RPKT_F_L4_SUM) {
-            uint16_t parts[2] = {oracle_pseudo_header_v4(ip + 12, ip + 16, 6, (uint16_t)l4len),
-                                 pbuf_from_buf(buf, l4len)};
-            rec->l4_sum = oracle_combine(parts, 2);
-        }
-        pbuf_advance(&buf, hl);                       /* Tcp::payload :125-131 */
-        rec->payload_off = (uint16_t)pbuf_cursor(&buf);
-        rec->payload_len = (uint16_t)pbuf_remaining(&buf);
-        rec->status = RPKT_S_OK;
-    } else {
-        rec->status = RPKT_S_L4_OTHER;
-    }
+    parse_pbuf_l4(&buf, ip[9], ip + 12, ip + 16, 0, flags, rec);
 }
 
 /* Load chain `first .. last-1` of the caller's segment list into `m`, clamping

@@ -42,6 +42,9 @@ MBUF_ROOM, MBUF_HEADROOM = 2048, 128                      # RTE_MBUF_DEFAULT_DAT
 # header-boundary cut positions for the chain fuzz (Ether 14, tags 18/22, IPv4 +20..60, L4 +8/20)
 FUZZ_CUTS = (0, 1, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 26, 30, 33, 34, 35, 38,
              42, 46, 54, 58, 62, 66, 74, 82, 94, 102, 118, 128, 142)
+# ... and for dual-stack configs the IPv6 ones (header 54/58/62 + 40, extension headers
+# of 8..24 B, the L4 header after them)
+FUZZ_CUTS6 = FUZZ_CUTS + (20, 53, 55, 56, 60, 70, 78, 86, 94, 96, 98, 102, 110, 126, 134, 150)
 
 _lib = None
 
@@ -143,13 +146,13 @@ def _mbuf_cuts(lens, room):
     return nseg, seg_len
 
 
-def _fuzz_cuts(lens, rng):
+def _fuzz_cuts(lens, rng, cuts_at=FUZZ_CUTS):
     nsegs, seg_lens = [], []
     for L in lens.tolist():
         k = int(rng.integers(1, 7))
         cuts = rng.integers(0, L + 1, size=k - 1).tolist()
         if k > 1 and rng.integers(0, 2):
-            cuts[0] = min(FUZZ_CUTS[int(rng.integers(0, len(FUZZ_CUTS)))], L)
+            cuts[0] = min(cuts_at[int(rng.integers(0, len(cuts_at)))], L)
         cuts = sorted(cuts)
         edges = [0] + cuts + [L]
         nsegs.append(k)
@@ -172,7 +175,7 @@ def make_chains(config, n=None, seed=None, threads=None, layout=None):
         nseg, seg_len = _mbuf_cuts(lens, MBUF_ROOM)
         slot_bytes, pad = MBUF_ROOM + MBUF_HEADROOM, np.full(seg_len.size, MBUF_HEADROOM)
     else:
-        nseg, seg_len = _fuzz_cuts(lens, rng)
+        nseg, seg_len = _fuzz_cuts(lens, rng, FUZZ_CUTS6 if config in DUAL_STACK else FUZZ_CUTS)
         slot_bytes, pad = 0, rng.integers(0, 64, size=seg_len.size)
     n_segs = seg_len.size
     chain_first = np.zeros(n + 1, dtype=np.int64)

@@ -10,7 +10,8 @@ for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact c5_opts c5_opts_compact wa
     P=$G/prof_$t; D=$R/profiles/${RND}_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
-    for k in fetch write; do
+    for k in fetch write rdreq; do
+        [ -f "$P/${k}_counter_collection.csv" ] || continue
         [ -f "$P/${k}_bench.log" ] && cp "$P/${k}_bench.log" "$D/"
         python3 "$R/tools/pmc_by_kernel.py" "$P/${k}_counter_collection.csv" > "$D/${k}_by_kernel.json"
     done

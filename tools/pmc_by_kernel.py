@@ -15,11 +15,16 @@ def main(path, skip=2):
     by = collections.defaultdict(list)
     with open(path) as fh:
         for r in csv.DictReader(fh):
-            by[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            by[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    counters = {c for _, c in by}
     out = {}
-    for k, v in by.items():
+    for (k, c), v in by.items():
         v = v[skip:] or v
-        out[k[:90]] = {"dispatches": len(v), "avg": sum(v) / len(v)}
+        row = {"dispatches": len(v), "avg": sum(v) / len(v)}
+        if len(counters) == 1:                     # one counter per pass: keyed by kernel
+            out[k[:90]] = row
+        else:                                      # several (the rdreq pass): kernel -> counter
+            out.setdefault(k[:90], {})[c] = row
     print(json.dumps(out, indent=1))
 
 
