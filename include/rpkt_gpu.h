@@ -357,7 +357,9 @@ typedef struct rpkt_chains {
  * each view's tests taken as they are over a Pbuf: header sizes against chunk() (the
  * rest of the segment holding the header's first byte; Pbuf::new starts at segment 0
  * even when it is empty), totals against remaining(), the packet end cut by the
- * IPv4/UDP trim_off.  Record offsets are logical positions in the chain's bytes,
+ * IPv4/IPv6/UDP trim_off.  With RPKT_F_IPV6 the IPv6 chain too: the 40-byte header and
+ * each extension header tested against its own chunk.  Record offsets are logical
+ * positions in the chain's bytes,
  * frame_len = pkt_len, l4_sum = from_buf over the segments (rpkt/src/checksum.rs:8-27).
  * The caller's segments are never modified (the reference's trim_off truncates the
  * mbuf chain, mbuf.rs:346-382).  recs_dev n_chains * 80 B, 16-byte aligned. */

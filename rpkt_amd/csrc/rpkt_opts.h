@@ -84,10 +84,9 @@ __device__ __forceinline__ uint32_t opt_rule_alu(bool tcp, uint32_t t) {
 // Both iterators' rule tables (IPv4: [0, 256), TCP: [256, 512)) into the block's LDS;
 // the caller synchronises the block before the walks read them.
 __device__ __forceinline__ void opt_rules_fill(uint8_t* rules) {
-    static_assert(kWave * kWavesPerBlock >= 256, "one fill pass");
-    if (threadIdx.x < 256) {
-        rules[threadIdx.x] = (uint8_t)opt_rule(false, threadIdx.x);
-        rules[256 + threadIdx.x] = (uint8_t)opt_rule(true, threadIdx.x);
+    for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x) {   // any block size
+        rules[t] = (uint8_t)opt_rule(false, t);
+        rules[256 + t] = (uint8_t)opt_rule(true, t);
     }
 }
 

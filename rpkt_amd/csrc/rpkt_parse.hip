@@ -197,7 +197,12 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     }
 }
 
-// WPB: waves per block (a block's slot on its CU is freed when its last wave ends)
+// WPB: waves per block (a block's slot on its CU is freed when its last wave ends);
+// the receive entries launch kParseWPB
+#ifndef RPKT_PARSE_WPB
+#define RPKT_PARSE_WPB 4
+#endif
+constexpr int kParseWPB = RPKT_PARSE_WPB;
 template <bool L4, int V, bool C16 = false, bool OPTS = false, int WPB = kWavesPerBlock>
 __global__ __launch_bounds__(kWave * WPB, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
@@ -323,6 +328,93 @@ __device__ __forceinline__ uint32_t chain_chunk(const ChainSrc& S, uint32_t a, u
     return 0;
 }
 
+// Chain bytes at absolute a..a+3 as a little-endian dword: from segment 0's LDS window
+// when they lie in its windowed part (frame bytes [0, lim) of segment 0), else byte-wise
+// from global memory.  A header lies inside the chunk it was tested against, i.e. in one
+// segment, so its bytes are at consecutive absolute addresses.
+struct ChainDw {
+    const uint8_t* slot;
+    uint32_t ph, off0, lim;
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ uint32_t operator()(uint32_t a) const {
+        const uint32_t x = a - off0;                           // wraps for other segments
+        if (x < lim && lim - x >= 4u) {
+            const uint32_t y = ph + x, q = y & ~3u;
+            return align_bytes(lds32(slot, q + 4), lds32(slot, q), y & 3u);
+        }
+        return gbyte(rs, a) | (gbyte(rs, a + 1) << 8) | (gbyte(rs, a + 2) << 16) |
+               (gbyte(rs, a + 3) << 24);
+    }
+};
+
+// parse_ip6 (rpkt_common.h) over a Pbuf: every header size against chunk().len() at its
+// first byte (the rest of the segment holding it, cut at the packet end), the payload
+// length against remaining() (ipv6/generated.rs:40-92 and the extension headers'
+// parses, as oracle/rpkt_oracle_chain.c parse_pbuf_ip6).
+__device__ __forceinline__ uint32_t parse_chain_ip6(const ChainDw& dw, uint32_t C, uint32_t pkt,
+                                                    const ChainSrc& S, uint32_t a, uint32_t b,
+                                                    uint32_t l3, uint32_t* w, uint32_t& l4,
+                                                    uint32_t& l4rem, uint32_t& proto,
+                                                    uint32_t& paddr) {
+    // chunk at logical cursor c under the packet end `lim`, its first byte's address
+    auto chunk = [&](uint32_t c, uint32_t lim, uint32_t& abs) -> uint32_t {
+        if (c < C) {
+            abs = dw.off0 + c;
+            return (C < lim ? C : lim) - c;
+        }
+        abs = S.fb;
+        return c < lim ? chain_chunk(S, a, b, c, lim, abs) : 0u;
+    };
+    uint32_t ab3;
+    if (chunk(l3, pkt, ab3) < 40u) return RPKT_S_IP6_SHORT;               // :42
+    uint32_t F[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) F[k] = dw(ab3 + 4u * k);
+    const uint32_t plen = be16_lo(F[1]);
+    if (plen + 40u > pkt - l3) return RPKT_S_IP6_BAD_LEN;                 // :47
+    w[6] = bswap32(F[0]);
+    w[7] = plen | (F[1] & 0xffff0000u);
+    w[9] = bswap32(F[2]) ^ bswap32(F[3]) ^ bswap32(F[4]) ^ bswap32(F[5]);
+    w[10] = bswap32(F[6]) ^ bswap32(F[7]) ^ bswap32(F[8]) ^ bswap32(F[9]);
+    const uint32_t src_sum = addr_words_sum(F[2], F[3], F[4], F[5]);
+    uint32_t pdst_sum = addr_words_sum(F[6], F[7], F[8], F[9]);
+    uint32_t pdst_off = l3 + 24u;
+    uint32_t c = l3 + 40u;
+    const uint32_t end = c + plen;                                        // payload() trim
+    uint32_t nh = (F[1] >> 16) & 0xffu, n_ext = 0, status = RPKT_S_OK;
+    for (int k = 0; k < RPKT_MAX_IP6_EXT && is_ip6_ext(nh); ++k) {
+        const bool fg = nh == 44u, ah = nh == 51u, rt = nh == 43u;
+        const uint32_t fixed = (nh == 0u || nh == 60u) ? 2u : (ah ? 12u : 8u);
+        uint32_t ax;
+        const uint32_t cl = chunk(c, end, ax);
+        if (cl < fixed) { status = RPKT_S_IP6_EXT_SHORT; break; }
+        const uint32_t d0 = dw(ax);
+        const uint32_t b1 = (d0 >> 8) & 0xffu;
+        const uint32_t hl = fg ? 8u : (ah ? b1 * 4u + 8u : b1 * 8u + 8u);
+        if (!fg && (hl < fixed || hl > cl)) { status = RPKT_S_IP6_EXT_BAD_LEN; break; }
+        if (rt && (d0 >> 24) != 0u) {
+            const uint32_t type = (d0 >> 16) & 0xffu, n_addr = (hl - 8u) >> 4;
+            if (n_addr != 0u && (type == 0u || type == 2u || type == 4u)) {
+                const uint32_t r = 8u + (type == 4u ? 0u : 16u * (n_addr - 1u));
+                pdst_off = c + r;
+                pdst_sum = addr_words_sum(dw(ax + r), dw(ax + r + 4u), dw(ax + r + 8u),
+                                          dw(ax + r + 12u));
+            }
+        }
+        nh = d0 & 0xffu;
+        c += hl;
+        n_ext += 1u;
+        if (fg && (be16_hi(d0) & 0xfff9u) != 0u) { status = RPKT_S_IP6_FRAGMENT; break; }
+    }
+    if (status == RPKT_S_OK && is_ip6_ext(nh)) status = RPKT_S_L4_OTHER;
+    w[8] = n_ext | (nh << 8) | (pdst_off << 16);
+    l4 = c;
+    l4rem = end - c;
+    proto = nh;
+    paddr = src_sum + pdst_sum;
+    return status;
+}
+
 // Lane-per-chain parse: parse_lane with the chunk/remaining distinction of a Pbuf.
 // C = segment 0's length: headers starting below C are read from the LDS window.
 __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane, Frame s0,
@@ -384,16 +476,34 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         c += 4;
     }
     w[0] = (nvlan << 8) | (eth_et << 16);
-    if (status == RPKT_S_OK && et != 0x0800u) status = RPKT_S_NOT_IPV4;
+    const bool v6 = (flags & RPKT_F_IPV6) && status == RPKT_S_OK && et == 0x86ddu;
+    if (status == RPKT_S_OK && et != 0x0800u && !v6) status = RPKT_S_NOT_IPV4;
     if (status != RPKT_S_OK) {
         w[0] |= status;
         L.status = status;
         return;
     }
 
-    // Ipv4::parse (ipv4/generated.rs:35-51): chunk vs remaining
     const uint32_t l3 = c;
     w[16] = l3;
+    uint32_t l4, limit, l4rem, proto, paddr;
+    if (v6) {
+        L.is6 = true;
+        const uint32_t wl = (uint32_t)kWin - ph;
+        const ChainDw dw{slot, ph, s0.off, C < wl ? C : wl, rs};
+        status = parse_chain_ip6(dw, C, pkt, S, a, b, l3, w, l4, l4rem, proto, paddr);
+        if (status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN) {
+            w[16] |= l4 << 16;
+            w[17] = (l4 & 0xffffu) | (l4rem << 16);
+        }
+        if (status != RPKT_S_OK) {
+            w[0] |= status;
+            L.status = status;
+            return;
+        }
+        limit = l4 + l4rem;
+    } else {
+    // Ipv4::parse (ipv4/generated.rs:35-51): chunk vs remaining
     Hdr6 ip;
     uint32_t ck3 = 0, ab3 = 0;
     const bool fast3 = l3 < C;
@@ -417,7 +527,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         L.status = status;
         return;
     }
-    const uint32_t proto = (ip.F[2] >> 8) & 0xffu;
+    proto = (ip.F[2] >> 8) & 0xffu;
     const uint32_t src = bswap32(ip.F[3]), dst = bswap32(ip.F[4]);
     w[6] = (ip.F[0] & 0xffffu) | (tot << 16);
     w[7] = be16_lo(ip.F[1]) | (be16_hi(ip.F[1]) << 16);
@@ -428,15 +538,19 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         w[18] = fast3 ? be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4),
                                s0.off + l3)
                       : gsum_be(rs, ab3, ihl4);
-    const uint32_t l4 = l3 + ihl4, limit = l3 + tot;           // Ipv4::payload :115-127
-    const uint32_t l4rem = tot - ihl4;
+    l4 = l3 + ihl4;                                            // Ipv4::payload :115-127
+    limit = l3 + tot;
+    l4rem = tot - ihl4;
     w[16] |= l4 << 16;
     w[17] = l4 | (l4rem << 16);
+    paddr = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu);
+    }
 
-    // Udp::parse / Tcp::parse against the chunk at l4 under the trimmed end
+    // Udp::parse / Tcp::parse against the chunk at l4 under the trimmed end (an IPv6 L4
+    // header past segment 0's window is read from global memory)
     Hdr6 h4;
     uint32_t ck4 = 0, ab4 = 0;
-    const bool fast4 = l4 < C;
+    const bool fast4 = l4 < C && ph + l4 + 20u <= (uint32_t)kWin;
     if (fast4) {
         ck4 = (C < limit ? C : limit) - l4;
         read_hdr(slot, ph + l4, h4);
@@ -453,7 +567,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
             w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
             w[14] = ulen;
             w[15] = be16_hi(h4.F[1]);
-            w[17] = (l4 + 8) | ((ulen - 8) << 16);
+            w[17] = ((l4 + 8) & 0xffffu) | ((ulen - 8) << 16);
             l4len = ulen;
         }
     } else if (proto == 6u) {
@@ -466,7 +580,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
             w[13] = bswap32(h4.F[2]);
             w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
             w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
-            w[17] = (l4 + hl) | ((l4rem - hl) << 16);
+            w[17] = ((l4 + hl) & 0xffffu) | ((l4rem - hl) << 16);
             l4len = l4rem;
         }
     } else {
@@ -476,7 +590,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
     L.status = status;
     if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
         L.want_l4 = true;
-        L.pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto + l4len;
+        L.pseudo = paddr + proto + l4len;
         const uint32_t e = l4 + l4len;
         L.l4_start_abs = s0.off + l4;                          // segment 0's byte phase
         if (fast4) {
@@ -1019,10 +1133,10 @@ int parse_options(const rpkt_batch_t* b, uint32_t flags, void* recs_dev, rpkt_op
     if (ok != 1) return ok;
     if (((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, C16, true>
-                                     : parse_kernel<false, 0, C16, true>;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, C16, true, kParseWPB>
+                                     : parse_kernel<false, 0, C16, true, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets, opts_dev);
@@ -1103,9 +1217,10 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
     const rpkt_batch_t* b, uint32_t flags, rpkt_rec16_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
     uint32_t n_buckets, void* stream) {
     const uint32_t flen = b->frame_len ? b->frame_len : b->stride;
-    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true, false, kParseWPB>
+                                     : parse_kernel<false, 0, true, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,
@@ -1152,9 +1267,10 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
         if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
     }
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0> : parse_kernel<false, 0>;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, false, false, kParseWPB>
+                                     : parse_kernel<false, 0, false, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
@@ -1195,9 +1311,10 @@ int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     if (RPKT_PARSE_W64_ON && parse_w64_fits(b, flen))
         return rpkt_gpu_parse_batch_compact_w64(b, flags, recs_dev, flow_ev_dev, n_buckets, stream);
-    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true> : parse_kernel<false, 0, true>;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true, false, kParseWPB>
+                                     : parse_kernel<false, 0, true, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,
@@ -1220,8 +1337,7 @@ int rpkt_gpu_parse_options_batch_compact(const rpkt_batch_t* b, uint32_t flags,
 int rpkt_gpu_parse_chains(const rpkt_chains_t* c, uint32_t flags, rpkt_rec_t* recs_dev,
                           rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!c || !recs_dev) return RPKT_E_INVAL;
-    // the chain parse is IPv4-only (RPKT_F_IPV6 is not accepted)
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV)) return RPKT_E_INVAL;
+    if (flags & ~kParseFlags) return RPKT_E_INVAL;
     if (c->n_chains == 0) return RPKT_OK;
     if (!c->chain_first_dev || (c->n_segs && (!c->buf_dev || !c->segs_dev))) return RPKT_E_INVAL;
     if (c->buf_bytes > kMaxFrameBytes || c->n_segs >= 0x80000000u) return RPKT_E_TOO_LARGE;

@@ -185,13 +185,6 @@ def test_build_skips_ip6_records(torch):
     assert np.array_equal(db.frames.cpu().numpy(), want_frames)
 
 
-def test_chains_refuse_the_ipv6_flag(torch):
-    hc = gen.make_chains(8, 100)
-    dc = engine.DeviceChains.from_host(hc)
-    with pytest.raises(engine.RpktError):
-        engine.parse_chains(dc, F6)
-
-
 def test_short_strided_ip6_frames(torch):
     """Strided 64/48/49-B slots of dual-stack fuzz frames: the compact parse of frames
     inside a 64-B window runs the 64-B-window compile."""
