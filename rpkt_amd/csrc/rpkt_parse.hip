@@ -197,10 +197,14 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     }
 }
 
-// WPB: waves per block (a block's slot on its CU is freed when its last wave ends);
-// the receive entries launch kParseWPB
+// WPB: waves per block.  A block's slot on its CU is freed only when its last wave
+// ends, and a config-2 wave lasts 3.7-7.3 us (tools/launch_stamps.py), so one-wave
+// blocks keep more waves in flight: the batch and compact entries launch kParseWPB = 1
+// (config 2: 27.0 -> 25.9 and 27.5 -> 26.1 us, compact 15.8 -> 15.5 us, config 3 the
+// same; profiles/r04_wpb/).  The fused option walks keep 4 (their 512-B rule table is
+// filled per block: 689 -> 701 us with one-wave blocks).
 #ifndef RPKT_PARSE_WPB
-#define RPKT_PARSE_WPB 4
+#define RPKT_PARSE_WPB 1
 #endif
 constexpr int kParseWPB = RPKT_PARSE_WPB;
 template <bool L4, int V, bool C16 = false, bool OPTS = false, int WPB = kWavesPerBlock>
@@ -264,13 +268,17 @@ struct RingArgs {
     RingSlot s[kRingMax];
 };
 
+#ifndef RPKT_RING_WPB
+#define RPKT_RING_WPB 4
+#endif
+constexpr int kRingWPB = RPKT_RING_WPB;                           // waves per block
 template <bool L4, bool C16>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+__global__ __launch_bounds__(kWave * kRingWPB, 4)
 void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
-    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch[kRingWPB];
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t t = blockIdx.x * kWavesPerBlock + wid;
+    const uint32_t t = blockIdx.x * kRingWPB + wid;
     if (t >= A.tile0[A.n_slots]) return;                          // wave-uniform exit
     uint32_t k = 0;                                               // the slot holding tile t
     for (uint32_t j = 1; j < A.n_slots; ++j) k = A.tile0[j] <= t ? j : k;
@@ -1133,10 +1141,10 @@ int parse_options(const rpkt_batch_t* b, uint32_t flags, void* recs_dev, rpkt_op
     if (ok != 1) return ok;
     if (((uintptr_t)opts_dev & 15u) != 0) return RPKT_E_ALIGN;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    const uint32_t per_block = kWave * kParseWPB;
+    const uint32_t per_block = kWave * kWavesPerBlock;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, C16, true, kParseWPB>
-                                     : parse_kernel<false, 0, C16, true, kParseWPB>;
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, C16, true>
+                                     : parse_kernel<false, 0, C16, true>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets, opts_dev);
@@ -1184,9 +1192,8 @@ int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
         }
         if (A.n_slots == 0) break;
         const uint32_t waves = A.tile0[A.n_slots];
-        const int rc = launch(k, dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock),
-                              dim3(kWave * kWavesPerBlock), 0, (hipStream_t)stream, A, flags,
-                              n_buckets);
+        const int rc = launch(k, dim3((waves + kRingWPB - 1) / kRingWPB), dim3(kWave * kRingWPB),
+                              0, (hipStream_t)stream, A, flags, n_buckets);
         if (rc) return rc;
     }
     return RPKT_OK;

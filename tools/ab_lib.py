@@ -3,7 +3,8 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7]
+Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7|ring2|ringc2]
+(ring<cfg> / ringc<cfg>: the R rotated batches as one rpkt_gpu_parse_ring[_compact] launch)
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
   python tools/ab_lib.py --build <out_dir> [hipcc -D flags ...]
@@ -114,6 +115,21 @@ def main():
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
             call[name] = (lambda k, L=L, out=out: L.rpkt_gpu_layers_batch(
                 ctypes.byref(descs[k % R]), out.data_ptr(), sp))
+        elif mode in ("ring", "ringc"):             # the R batches as one parse_ring launch
+            c16 = mode == "ringc"
+            rr = [torch.zeros(h.n * (16 if c16 else 80), dtype=torch.uint8, device="cuda")
+                  for h in hbs]
+            ring = engine.ring_slots(dbs, rr)
+            fn = L.rpkt_gpu_parse_ring_compact if c16 else L.rpkt_gpu_parse_ring
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                           ctypes.c_void_p]
+            flags = 1 if cfg == 2 else 3
+            keep_alive.append((rr, ring))
+            out = rr[0]
+            for r in range(1, R):
+                outs["%s_ring%d" % (name, r)] = rr[r]
+            call[name] = (lambda k, fn=fn, ring=ring, flags=flags: fn(
+                ctypes.cast(ring, ctypes.c_void_p), len(ring), flags, 0, sp))
         elif mode == "parse":
             L.rpkt_gpu_parse_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p]
