@@ -268,10 +268,12 @@ struct RingArgs {
     RingSlot s[kRingMax];
 };
 
+// waves per block of the ring launch: one, as the batch entries (8-slot ring of config
+// 2: 195.8 -> 193.0 us, compact 109.0 -> 103.2 us; profiles/r04_wpb/ab_ring1.jsonl)
 #ifndef RPKT_RING_WPB
-#define RPKT_RING_WPB 4
+#define RPKT_RING_WPB 1
 #endif
-constexpr int kRingWPB = RPKT_RING_WPB;                           // waves per block
+constexpr int kRingWPB = RPKT_RING_WPB;
 template <bool L4, bool C16>
 __global__ __launch_bounds__(kWave * kRingWPB, 4)
 void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {

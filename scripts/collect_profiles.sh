@@ -6,7 +6,7 @@ set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
 RND=${RND:-r02}
-for t in ${TAGS:-c2 c3 c4 c5 c7 c2_compact c3_compact c5_opts c5_opts_compact walks build3 optsc5}; do
+for t in ${TAGS:-c2 c3 c4 c5 c7 c10 c11 c2_compact c3_compact c11_compact c5_opts c5_opts_compact walks build3 optsc5}; do
     P=$G/prof_$t; D=$R/profiles/${RND}_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
