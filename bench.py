@@ -45,7 +45,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from rpkt_amd import dist as rdist, engine, fields, gen  # noqa: E402
-from rpkt_amd.records import LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, as_records  # noqa: E402,E501
+from rpkt_amd.records import (LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, as_records,  # noqa: E402
+                              is_ip6)
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -899,12 +900,12 @@ def run_tx(cfg, mode, args, rank, world):
     r = as_records(recs[0].cpu().numpy())
     lens = hbs[0].lens()
     fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
-    if mode == "build":
-        alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
     floor = None                               # the 128-B line floor of the reads + writes
     fo = hbs[0].offsets[:-1].astype(np.int64) if hbs[0].offsets is not None else \
         np.arange(hbs[0].n, dtype=np.int64) * hbs[0].stride
-    if mode == "layers":                       # header bytes walked + 64 B out per frame
+    if mode == "build":
+        alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
+    elif mode == "layers":                       # header bytes walked + 64 B out per frame
         lo = outs[0].cpu().numpy().view(LAYERS_DTYPE)
         walked = np.minimum(lo["payload_off"].astype(np.int64), lens)
         alg = int(walked.sum()) + hbs[0].n * 64
@@ -916,7 +917,7 @@ def run_tx(cfg, mode, args, rank, world):
         got = sum(int(((pm >> r) & 1).sum()) * nb for r, nb in enumerate(nbytes))
         alg = hbs[0].n * (64 + 8 * len(reqs) + 4) + got
     elif mode in ("opts", "optsc"):            # records + option slices read, 64 B written
-        ip_parsed = (r["status"] == 0) | (r["status"] >= 9)
+        ip_parsed = ((r["status"] == 0) | (r["status"] >= 9)) & ~is_ip6(r)   # Ipv4OptionsIter
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
         l3, l4 = r["l3_off"].astype(np.int64), r["l4_off"].astype(np.int64)
         po = r["payload_off"].astype(np.int64)
