@@ -916,6 +916,23 @@ def run_tx(cfg, mode, args, rank, world):
                   for q in reqs]
         got = sum(int(((pm >> r) & 1).sum()) * nb for r, nb in enumerate(nbytes))
         alg = hbs[0].n * (64 + 8 * len(reqs) + 4) + got
+        # the lines holding the fields read: each present request's bytes at the offset of
+        # the nth layer of its protocol (rpkt_gpu_fields_batch's rule)
+        lay = lays[0].cpu().numpy().view(LAYERS_DTYPE)
+        live = np.arange(16)[None, :] < lay["n"].astype(np.int64)[:, None]
+        rows = np.arange(hbs[0].n)
+        s0, s1 = [], []
+        for r, q in enumerate(reqs):
+            hit = (lay["proto"] == q["proto"]) & live
+            sel = hit & (np.cumsum(hit, axis=1) == int(q["nth"]) + 1)
+            has = sel.any(axis=1) & (((pm >> r) & 1) != 0)
+            off = lay["off"][rows, sel.argmax(axis=1)].astype(np.int64)
+            b0 = off + int(q["bit_off"]) // 8
+            b1 = off + (int(q["bit_off"]) + int(q["bits"]) - 1) // 8 + 1
+            s0.append(np.where(has, fo + b0, 0))
+            s1.append(np.where(has, fo + b1, 0))
+        floor = hbs[0].n * (64 + 8 * len(reqs) + 4) + line_floor(np.concatenate(s0),
+                                                                 np.concatenate(s1))
     elif mode in ("opts", "optsc"):            # records + option slices read, 64 B written
         ip_parsed = ((r["status"] == 0) | (r["status"] >= 9)) & ~is_ip6(r)   # Ipv4OptionsIter
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
