@@ -661,30 +661,56 @@ __device__ __forceinline__ uint32_t raw_range_sum(const uint8_t* slot, const uin
 
 __device__ __forceinline__ bool is_tag(uint32_t et) { return et == 0x8100u || et == 0x88a8u; }
 
-// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout),
-// byte loads: the rare paths whose header lies outside the LDS window
-__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint32_t (&F)[5]) {
+// Buffer bytes a..a+3 as a little-endian dword: two aligned dword loads and a byte
+// align (bytes past the buffer read as 0, as gbyte's: the buffer's last, partial dword
+// byte-wise)
+__device__ __forceinline__ uint32_t gdword(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t a) {
+    const uint32_t a4 = a & ~3u;
+    auto ld = [&](uint32_t x) -> uint32_t {
+        if (__builtin_expect(x + 4u <= fb, 1))
+            return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)x, 0, 0);
+        return gbyte(rs, x) | (gbyte(rs, x + 1u) << 8) | (gbyte(rs, x + 2u) << 16) |
+               (gbyte(rs, x + 3u) << 24);
+    };
+    return align_bytes(ld(a4 + 4u), ld(a4), a & 3u);
+}
+
+// 20 bytes at absolute `a` as frame-relative little-endian dwords (Hdr6::F layout): the
+// rare paths whose header lies outside the LDS window.  Six aligned dword loads in one
+// round trip; near the buffer's end, bytes.
+__device__ __forceinline__ void gread20(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t a,
+                                        uint32_t (&F)[5]) {
+    const uint32_t a4 = a & ~3u, sh = a & 3u;
+    uint32_t R[6];
+    if (__builtin_expect(a4 + 24u <= fb, 1)) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k)
-        F[k] = gbyte(rs, a + 4 * k) | (gbyte(rs, a + 4 * k + 1) << 8) |
-               (gbyte(rs, a + 4 * k + 2) << 16) | (gbyte(rs, a + 4 * k + 3) << 24);
+        for (int k = 0; k < 6; ++k)
+            R[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(a4 + 4u * k), 0, 0);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t x = a4 + 4u * k;
+            R[k] = gbyte(rs, x) | (gbyte(rs, x + 1) << 8) | (gbyte(rs, x + 2) << 16) |
+                   (gbyte(rs, x + 3) << 24);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) F[k] = align_bytes(R[k + 1], R[k], sh);
 }
 
 // Frame bytes x..x+3 of a lane's frame as a little-endian dword: from its LDS window
-// slot when they lie in the window, else byte-wise from global memory (IPv6 extension
-// headers past the window; bytes past the buffer read as 0).
+// slot when they lie in the window, else from global memory (IPv6 extension headers
+// past the window; bytes past the buffer read as 0).
 struct FrameDw {
     const uint8_t* slot;
-    uint32_t ph, off;
+    uint32_t ph, off, fb;
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ uint32_t operator()(uint32_t x) const {
         if (__builtin_expect(ph + x + 4u <= (uint32_t)kWin, 1)) {
             const uint32_t y = ph + x, a = y & ~3u;
             return align_bytes(lds32(slot, a + 4), lds32(slot, a), y & 3u);
         }
-        const uint32_t g = off + x;
-        return gbyte(rs, g) | (gbyte(rs, g + 1) << 8) | (gbyte(rs, g + 2) << 16) |
-               (gbyte(rs, g + 3) << 24);
+        return gdword(rs, fb, off + x);
     }
 };
 
@@ -708,7 +734,8 @@ __device__ __forceinline__ bool is_ip6_ext(uint32_t nh) {
 // Returns the status; on OK: l4 (frame offset of the upper-layer header), its
 // remaining bytes, the protocol and the pseudo header's address sum.
 __device__ __forceinline__ uint32_t parse_ip6(const uint8_t* slot, uint32_t ph, Frame fr,
-                                              __amdgpu_buffer_rsrc_t rs, uint32_t l3, uint32_t rem,
+                                              __amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                              uint32_t l3, uint32_t rem,
                                               uint32_t* w, uint32_t& l4, uint32_t& l4rem,
                                               uint32_t& proto, uint32_t& paddr) {
     if (rem < 40u) return RPKT_S_IP6_SHORT;                               // :42
@@ -730,7 +757,7 @@ __device__ __forceinline__ uint32_t parse_ip6(const uint8_t* slot, uint32_t ph, 
     const uint32_t src_sum = addr_words_sum(F[2], F[3], F[4], F[5]);
     uint32_t pdst_sum = addr_words_sum(F[6], F[7], F[8], F[9]);
     uint32_t pdst_off = l3 + 24u;
-    const FrameDw dw{slot, ph, fr.off, rs};
+    const FrameDw dw{slot, ph, fr.off, fb, rs};
     uint32_t c = l3 + 40u;
     const uint32_t end = c + plen;
     uint32_t nh = (F[1] >> 16) & 0xffu, n_ext = 0, status = RPKT_S_OK;
@@ -773,7 +800,7 @@ __device__ __forceinline__ uint32_t parse_ip6(const uint8_t* slot, uint32_t ph, 
 // LDS dword reads: link layer (bytes 0..23), IPv4 header at l3, L4 header at l4.
 __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame fr, bool valid,
                                            uint32_t flags, LaneRec& L,
-                                           __amdgpu_buffer_rsrc_t rs) {
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t fb) {
     const uint32_t ph = fr.off & 15u;
     const uint8_t* slot = &W.win[lane * kSlot];
     uint32_t* w = L.w;
@@ -843,7 +870,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     if (v6) {
         // round 2 (IPv6): the header, the extension headers, the pseudo header's addresses
         L.is6 = true;
-        status = parse_ip6(slot, ph, fr, rs, l3, rem, w, l4, l4rem, proto, paddr);
+        status = parse_ip6(slot, ph, fr, rs, fb, l3, rem, w, l4, l4rem, proto, paddr);
         if (status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN) {
             w[16] |= l4 << 16;
             w[17] = (l4 & 0xffffu) | (l4rem << 16);
@@ -893,7 +920,10 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     // in-window part of its sum is whatever of it the window holds.
     Hdr6 h4;
     read_hdr(slot, v6 && ph + l4 > (uint32_t)kWin ? (uint32_t)kWin : ph + l4, h4);
-    if (v6 && __builtin_expect(ph + l4 + 20u > (uint32_t)kWin, 0)) gread20(rs, fr.off + l4, h4.F);
+    // (a UDP header needs only its 8 bytes in the window: the 64-B-window compile keeps
+    // an untagged IPv6/UDP frame's header, bytes 54..61, in LDS)
+    if (v6 && __builtin_expect(ph + l4 + (proto == 17u ? 8u : 20u) > (uint32_t)kWin, 0))
+        gread20(rs, fb, fr.off + l4, h4.F);
     uint32_t l4len = 0;
     if (proto == 17u) {
         const uint32_t ulen = be16_lo(h4.F[1]);

@@ -161,27 +161,6 @@ __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto,
     return S;
 }
 
-// ---- Ipv6OptionsIter over the extension chain (the IPv6 half of rpkt_opts_t) ----
-// Ipv6OptionsIter::next (ipv6/generated.rs:1568-1615) over the var_header_slice() of every
-// HopByHopOption / DestOptions header (:384-412, :241-269) of the chain the parse walked,
-// frame bytes [l3 + 40, l4), in order; a malformed option ends the walking.  Pad0 (0) is
-// one byte; PadN (1) and Generic (2..4, 6..255): chunk >= 2 and header_len = b1 + 2 <=
-// chunk; RouterAlert (5): chunk >= 4 and header_len == 4.  A lane walks its own frame from
-// global memory (the bytes were just fetched by the window or the refill, so mostly L2
-// hits): the chain can run far past the 128-B window (a HopByHop header alone may hold
-// 2048 B), and few frames carry options headers.  Writes words 7..11, 14, 15 and byte 27
-// of the frame's 64-B row (include/rpkt_gpu.h, the IPv6 view).
-__device__ __forceinline__ uint32_t gdword(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t a) {
-    const uint32_t a4 = a & ~3u;
-    auto ld = [&](uint32_t x) -> uint32_t {
-        if (__builtin_expect(x + 4u <= fb, 1))
-            return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)x, 0, 0);
-        return gbyte(rs, x) | (gbyte(rs, x + 1u) << 8) | (gbyte(rs, x + 2u) << 16) |
-               (gbyte(rs, x + 3u) << 24);      // the buffer's last, partial dword
-    };
-    return align_bytes(ld(a4 + 4u), ld(a4), a & 3u);
-}
-
 __device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t fo,
                                              uint32_t l3, uint32_t l4, uint32_t* row) {
     uint32_t nh = (gdword(rs, fb, fo + l3 + 4u) >> 16) & 0xffu;   // next_header, byte 6

@@ -140,7 +140,7 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
         for (int k = 0; k < 20; ++k) L.w[k] = x + k;
         L.status = 0;
     } else {
-        parse_lane(W, lane, fr, valid, flags, L, rs);
+        parse_lane(W, lane, fr, valid, flags, L, rs, frames_bytes);
     }
     if constexpr (OPTS) options_from_window(W, rs, frames_bytes, lane, fr, L, opt_rules, opts, p0, n);
     if constexpr (V != 3 && !C16) stage_record(W, lane, L.w);
@@ -522,7 +522,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         read_hdr(slot, ph + l3, ip);
     } else {
         if (l3 < pkt) ck3 = chain_chunk(S, a, b, l3, pkt, ab3);
-        gread20(rs, ck3 ? ab3 : S.fb, ip.F);
+        gread20(rs, S.fb, ck3 ? ab3 : S.fb, ip.F);
     }
     const uint32_t vhl = ip.F[0] & 0xffu;
     const uint32_t ihl4 = (vhl & 0xfu) * 4u;
@@ -566,7 +566,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         read_hdr(slot, ph + l4, h4);
     } else {
         if (l4 < limit) ck4 = chain_chunk(S, a, b, l4, limit, ab4);
-        gread20(rs, ck4 ? ab4 : S.fb, h4.F);
+        gread20(rs, S.fb, ck4 ? ab4 : S.fb, h4.F);
     }
     uint32_t l4len = 0;
     if (proto == 17u) {

@@ -391,7 +391,8 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         return;
     }
     LaneRec L;
-    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L, rs);
+    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L, rs,
+               fb);
     uint8_t* slot = &W.win[lane * kSlot];
     uint8_t* s = slot + (fr.off & 15u);
     {

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--n", type=int, default=0, help="frames per batch (default: the config's)")
+    ap.add_argument("--flags", type=int, default=None,
+                    help="parse / ring flags (default: 1 for config 2, else 3)")
     ap.add_argument("--sides", default="AB",
                     help="sides to launch (a rocprofv3 --pmc pass of one build: A or B)")
     ap.add_argument("--rotate", type=int, default=0,
@@ -60,7 +62,7 @@ def main():
     A = engine.lib()
     B = ctypes.CDLL(os.path.abspath(args.lib_b))
     mode, cfg = args.leg.rstrip("0123456789"), int(args.leg[len(args.leg.rstrip("0123456789")):])
-    R = args.rotate or (8 if cfg == 2 else 1)    # 8 x 64 MiB of frames: past the 256 MiB cache
+    R = args.rotate or (8 if cfg in (2, 10) else 1)   # 8 x 64 MiB of frames: past the 256 MiB cache
     if mode == "chains":                         # mbuf chains (configs 7, 8)
         hbs = [gen.make_chains(cfg, args.n or None)]
         dbs = [engine.DeviceChains.from_host(h) for h in hbs]
@@ -123,7 +125,7 @@ def main():
             fn = L.rpkt_gpu_parse_ring_compact if c16 else L.rpkt_gpu_parse_ring
             fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                            ctypes.c_void_p]
-            flags = 1 if cfg == 2 else 3
+            flags = args.flags if args.flags is not None else (1 if cfg == 2 else 3)
             keep_alive.append((rr, ring))
             out = rr[0]
             for r in range(1, R):
@@ -134,7 +136,7 @@ def main():
             L.rpkt_gpu_parse_batch.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_uint32, ctypes.c_void_p]
             out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
-            flags = 1 if cfg == 2 else 3
+            flags = args.flags if args.flags is not None else (1 if cfg == 2 else 3)
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
         elif mode == "chains":                      # rpkt_gpu_parse_chains, both sums
@@ -149,7 +151,7 @@ def main():
                                                        ctypes.c_void_p, ctypes.c_uint32,
                                                        ctypes.c_void_p]
             out = torch.zeros(hb.n * 16, dtype=torch.uint8, device="cuda")
-            flags = 1 if cfg == 2 else 3
+            flags = args.flags if args.flags is not None else (1 if cfg == 2 else 3)
             call[name] = (lambda k, L=L, out=out, flags=flags: L.rpkt_gpu_parse_batch_compact(
                 ctypes.byref(descs[k % R]), flags, out.data_ptr(), None, 0, sp))
         elif mode == "fields":                      # bench.py's 16 getters over the walk
