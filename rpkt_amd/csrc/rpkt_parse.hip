@@ -91,7 +91,10 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
 // OPTS: also walk each frame's IPv4 and TCP options (rpkt_gpu_parse_options_batch) from
 // the header window the parse holds, between the parse and the L4 stream.
 // The tile of frames [p0, p0 + 64) of a batch, by one wave with its scratch W (p0 < n).
-template <bool L4, int V, bool C16, bool OPTS>
+// INWIN: every frame of the batch lies inside its header window (a strided batch of
+// short frames, window_fits), so the L4 sums are whole in LDS and step 3 (the edge lines
+// and the stream past the window) is compiled out.
+template <bool L4, int V, bool C16, bool OPTS, bool INWIN = false>
 __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_rules,
                                            const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                                            const uint32_t* __restrict__ offsets, uint32_t stride,
@@ -122,7 +125,7 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     // tiles streaming more than 32 KB sum their frames' edge lines with the window
     // (edge_lines_window; profiles/r02_edge_window: config 5 -1.2 % time and -9 % read
     // traffic, configs 3 and 4 unchanged in time; every tile: config 4 +10 %)
-    if constexpr (L4 && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
+    if constexpr (L4 && !INWIN && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
         X = edge_lines_window(rs, frames_bytes, W, lane, fr, valid,
                               V == 40 ? 0u : V == 41 ? 16384u : V == 43 ? 65536u : kEdgeWindowBytes);
     else if constexpr (L4 && V == 44)                  // the round-1 split: a pass after the window
@@ -150,9 +153,11 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     // keep the default policy (nt there measured slower).
     if (L4 && V != 1) {
         constexpr int kAux = (V == 22) ? 0 : 2;
-        uint32_t sp;
+        uint32_t sp = 0;
         const uint32_t ss = L.stream_s, se = L.stream_e;
-        if (V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes)) {
+        if constexpr (INWIN) {
+            (void)ss, (void)se;
+        } else if (V == 23 || (V == 25 && wave_sum(se - ss) > kSplitStreamBytes)) {
             // ablation: the same split taken after the parse
             const uint32_t h1 = min(se, (ss + 127u) & ~127u);
             const uint32_t t0 = max(se & ~127u, h1);
@@ -197,7 +202,7 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     }
 }
 
-// WPB: waves per block.  A block's slot on its CU is freed only when its last wave
+// INWIN: see parse_tile.  WPB: waves per block.  A block's slot on its CU is freed only when its last wave
 // ends, and a config-2 wave lasts 3.7-7.3 us (tools/launch_stamps.py), so one-wave
 // blocks keep more waves in flight: the batch and compact entries launch kParseWPB = 1
 // (config 2: 27.0 -> 25.9 and 27.5 -> 26.1 us, compact 15.8 -> 15.5 us, config 3 the
@@ -207,7 +212,8 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
 #define RPKT_PARSE_WPB 1
 #endif
 constexpr int kParseWPB = RPKT_PARSE_WPB;
-template <bool L4, int V, bool C16 = false, bool OPTS = false, int WPB = kWavesPerBlock>
+template <bool L4, int V, bool C16 = false, bool OPTS = false, int WPB = kWavesPerBlock,
+          bool INWIN = false>
 __global__ __launch_bounds__(kWave * WPB, 4)    // 4 waves/SIMD: <= 128 VGPRs
 void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
@@ -233,8 +239,9 @@ void parse_kernel(const uint8_t* __restrict__ frames, uint32_t frames_bytes,
     uint64_t t0 = 0;
     if constexpr (V == 50) t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    parse_tile<L4, V, C16, OPTS>(scratch[wid], opt_rules, frames, frames_bytes, offsets, stride,
-                                 frame_len, n, flags, recs, flow_ev, n_buckets, opts, p0, lane);
+    parse_tile<L4, V, C16, OPTS, INWIN>(scratch[wid], opt_rules, frames, frames_bytes, offsets,
+                                        stride, frame_len, n, flags, recs, flow_ev, n_buckets,
+                                        opts, p0, lane);
 #ifdef RPKT_ABLATE
     if constexpr (V == 50) {
         __builtin_amdgcn_s_waitcnt(0);
@@ -274,7 +281,7 @@ struct RingArgs {
 #define RPKT_RING_WPB 1
 #endif
 constexpr int kRingWPB = RPKT_RING_WPB;
-template <bool L4, bool C16>
+template <bool L4, bool C16, bool INWIN = false>
 __global__ __launch_bounds__(kWave * kRingWPB, 4)
 void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch[kRingWPB];
@@ -285,7 +292,7 @@ void parse_ring_kernel(const RingArgs A, uint32_t flags, uint32_t n_buckets) {
     uint32_t k = 0;                                               // the slot holding tile t
     for (uint32_t j = 1; j < A.n_slots; ++j) k = A.tile0[j] <= t ? j : k;
     const RingSlot& S = A.s[k];
-    parse_tile<L4, 0, C16, false>(scratch[wid], nullptr, S.frames, S.frames_bytes, S.offsets,
+    parse_tile<L4, 0, C16, false, INWIN>(scratch[wid], nullptr, S.frames, S.frames_bytes, S.offsets,
                                     S.stride, S.frame_len, S.n, flags, S.recs, S.flow_ev, n_buckets,
                                     nullptr, (t - A.tile0[k]) * kWave, lane);
 }
@@ -1117,6 +1124,14 @@ __global__ void chain_fold_kernel(const uint32_t* __restrict__ seg_out,
 // flags the batch / ring / fused-option parses accept
 constexpr uint32_t kParseFlags = RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_FLOW_EV | RPKT_F_IPV6;
 
+// every frame of a strided batch inside the header window from its 16-B boundary (the
+// frame at i * stride has phase (i * stride) & 15: 0 for strides of 16-B multiples)
+inline bool window_fits(const rpkt_batch_t& b, uint32_t win) {
+    const uint32_t flen = b.frame_len ? b.frame_len : b.stride;
+    if (b.offsets_dev || b.stride == 0 || flen == 0) return false;
+    return flen + ((b.stride & 15u) ? 15u : 0u) <= win;
+}
+
 // shared checks of the parse entry points
 int parse_args_ok(const rpkt_batch_t* b, uint32_t flags, const void* recs_dev,
                          const void* flow_ev_dev, uint32_t n_buckets) {
@@ -1170,7 +1185,12 @@ int parse_ring(const rpkt_ring_slot_t* slots, uint32_t n_slots, uint32_t flags,
         if (fev && !q.flow_ev_dev) return RPKT_E_INVAL;
         if (fev && ((uintptr_t)q.flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
     }
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_ring_kernel<true, C16> : parse_ring_kernel<false, C16>;
+    bool inwin = (flags & RPKT_F_L4_SUM) != 0;                    // every slot's frames in LDS
+    for (uint32_t k = 0; inwin && k < n_slots; ++k)
+        inwin = slots[k].batch.n == 0 || window_fits(slots[k].batch, (uint32_t)kWin);
+    auto k = !(flags & RPKT_F_L4_SUM) ? parse_ring_kernel<false, C16>
+           : inwin                    ? parse_ring_kernel<true, C16, true>
+                                      : parse_ring_kernel<true, C16>;
     RingArgs A;
     uint32_t k0 = 0;
     while (k0 < n_slots) {
@@ -1228,7 +1248,8 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
     const uint32_t flen = b->frame_len ? b->frame_len : b->stride;
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true, false, kParseWPB>
+    // the caller checked that every frame lies in its 64-B window: in-window L4 sums
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true, false, kParseWPB, true>
                                      : parse_kernel<false, 0, true, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
@@ -1278,8 +1299,9 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, false, false, kParseWPB>
-                                     : parse_kernel<false, 0, false, false, kParseWPB>;
+    auto k = !(flags & RPKT_F_L4_SUM)     ? parse_kernel<false, 0, false, false, kParseWPB>
+           : window_fits(*b, (uint32_t)kWin) ? parse_kernel<true, 0, false, false, kParseWPB, true>
+                                            : parse_kernel<true, 0, false, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
@@ -1322,8 +1344,9 @@ int rpkt_gpu_parse_batch_compact(const rpkt_batch_t* b, uint32_t flags, rpkt_rec
         return rpkt_gpu_parse_batch_compact_w64(b, flags, recs_dev, flow_ev_dev, n_buckets, stream);
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, true, false, kParseWPB>
-                                     : parse_kernel<false, 0, true, false, kParseWPB>;
+    auto k = !(flags & RPKT_F_L4_SUM)     ? parse_kernel<false, 0, true, false, kParseWPB>
+           : window_fits(*b, (uint32_t)kWin) ? parse_kernel<true, 0, true, false, kParseWPB, true>
+                                            : parse_kernel<true, 0, true, false, kParseWPB>;
     return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,

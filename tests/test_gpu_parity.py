@@ -351,11 +351,15 @@ def test_compact_fixtures_alignment(torch, lead):
 # ---- strided batches of short frames at every stride phase -----------------------------
 
 @pytest.mark.parametrize("stride,flen", [(64, 64), (64, 60), (64, 14), (48, 48), (49, 49),
-                                         (40, 40), (80, 64), (32, 20), (64, 65), (96, 96)])
+                                         (40, 40), (80, 64), (32, 20), (64, 65), (96, 96),
+                                         (112, 112), (128, 128), (113, 113), (129, 129),
+                                         (144, 128)])
 def test_short_strided_frames(torch, stride, flen):
     """Strided batches of short frames (strides that are and are not multiples of 16, so
     every 16-B phase of a window occurs): fuzzed headers of every status cut to flen
-    bytes, records bit-exact vs the oracle, full and compact."""
+    bytes, records bit-exact vs the oracle, full and compact.  Batches whose frames all
+    lie in their 128-B (64-B) windows take the in-window L4 instantiation (no stream
+    past the window); (129, 129) and (64, 65) just miss it."""
     from rpkt_amd.records import project16
     src = gen.make_batch(6, 20000, seed=stride * 131 + flen)
     n = src.n
@@ -376,3 +380,33 @@ def test_short_strided_frames(torch, stride, flen):
     o, oev = oracle_records(hb, 3, 4096, flow=True)
     assert_same16(g, project16(o, 3))
     assert np.array_equal(gev, oev)
+
+
+@pytest.mark.parametrize("stride,flen", [(64, 64), (80, 80), (113, 113), (128, 128), (130, 130)])
+def test_short_strided_dual_stack(torch, stride, flen):
+    """The same over the dual-stack fuzz (IPv6 extension chains cut at any byte): full and
+    compact records, flow events, and a receive ring of such batches, against the oracle."""
+    from rpkt_amd.records import F_IPV6, project16
+    src = gen.make_batch(12, 12000, seed=stride * 7 + flen)
+    n = src.n
+    buf = np.zeros(n * stride + 64, dtype=np.uint8)
+    lens = src.lens()
+    for i in range(n):
+        a = int(src.offsets[i])
+        k = min(int(lens[i]), flen)
+        buf[i * stride:i * stride + k] = src.frames[a:a + k]
+    hb = gen.HostBatch(12, n, 0, buf, None, stride, flen)
+    for flags in (F_IPV6 | 3, F_IPV6 | 2):
+        o = oracle_records(hb, flags)
+        assert_same(gpu_records(hb, flags), o)
+        assert_same16(gpu_records16(hb, flags), project16(o, flags))
+    g, gev = gpu_records16(hb, F_IPV6 | 3 | F_FLOW_EV, 4096)
+    o, oev = oracle_records(hb, F_IPV6 | 3, 4096, flow=True)
+    assert_same16(g, project16(o, F_IPV6 | 3))
+    assert np.array_equal(gev, oev)
+    db = engine.DeviceBatch.from_host(hb)
+    recs = [engine.alloc_records(n), engine.alloc_records(n)]
+    engine.parse_ring(engine.ring_slots([db, db], recs), F_IPV6 | 3)
+    o = oracle_records(hb, F_IPV6 | 3)
+    for r in recs:
+        assert_same(as_records(r.cpu().numpy()), o)
