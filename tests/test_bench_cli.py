@@ -38,3 +38,23 @@ def test_tx_leg_names():
         bench.tx_legs("opts")
     ap_default = [a for a in open(bench.__file__).read().split("\n") if '"--tx", default=' in a][0]
     bench.tx_legs(ap_default.split('default="')[1].split('"')[0])
+
+
+def test_line_floor_matches_brute_force():
+    """bench.line_floor (the 128-B line floor of the walk legs' roofline): the bytes of
+    the distinct lines any range touches, against a set of line indices."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        n = int(rng.integers(0, 200))
+        s = rng.integers(0, 20000, n)
+        e = s + rng.integers(-5, 400, n)              # empty and negative ranges included
+        lines = set()
+        for a, b in zip(s.tolist(), e.tolist()):
+            if b > a:
+                lines.update(range(a // 128, (b - 1) // 128 + 1))
+        assert bench.line_floor(s, e) == 128 * len(lines)
+    assert bench.line_floor([], []) == 0
+    assert bench.line_floor([127], [129]) == 256 and bench.line_floor([128], [256]) == 128
