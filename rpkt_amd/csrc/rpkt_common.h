@@ -599,6 +599,74 @@ __device__ __forceinline__ void window_commit(WaveScratch& W, __amdgpu_buffer_rs
     }
 }
 
+// The window and the edge lines issued together (long tiles).  A frame's head edge
+// line is the line its window ends in, and its tail edge line the line the next frame's
+// window starts in; loaded in separate passes (edge_lines_window after window_commit),
+// the second touch of such a line comes microseconds after the first, when 512 waves
+// per XCD streaming their tiles have pushed it out of the 4-MB L2, and it is fetched
+// twice (config 3: reads 1.042x the frame bytes at stride 1500, 1.000x at stride 1536
+// where no line is shared; profiles/r04_fp/).  Here each load instruction group covers
+// eight frames' window, head and tail chunks at once (the same cooperative mapping:
+// chunk k of lane l is piece l % 8 of frame 8k + l / 8), in two halves of 12 loads.
+// Returns the same EdgeLines as edge_lines_window; the window lands in LDS as
+// window_commit leaves it.
+template <int AUX = 0>
+__device__ __forceinline__ EdgeLines window_with_edges(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                       WaveScratch& W, int lane, Frame fr,
+                                                       bool valid) {
+    static_assert(kWinChunks == 8, "the 128-B window compile");
+    const int j = lane & 7;
+    constexpr int kHalf = kWinChunks / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u32x4 dw[kHalf], dh[kHalf], dt[kHalf];
+        uint32_t aw[kHalf], ah[kHalf], at[kHalf], lh[kHalf], lt[kHalf];
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            const int k = h * kHalf + i;
+            const int q = (k * kWave + lane) >> 3;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t qn = (uint32_t)__shfl((int)fr.len, q, kWave);
+            const uint32_t ql = (uint32_t)__shfl((int)(valid ? fr.len : 0u), q, kWave);
+            const uint32_t a = (qo & ~15u) + 16u * j;                // window_issue's chunk
+            aw[i] = (a < qo + qn) ? a : fb;
+            uint32_t wend, fend, he, tb;
+            edge_spans(qo, ql, wend, fend, he, tb);
+            const uint32_t x = wend + 16u * j, y = tb + 16u * j;
+            const bool hin = x < he, tin = y < fend && tb < fend;
+            ah[i] = hin ? x : fb;
+            at[i] = tin ? y : fb;
+            lh[i] = hin ? (he - x < 16u ? he - x : 16u) : 0u;
+            lt[i] = tin ? (fend - y < 16u ? fend - y : 16u) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            dw[i] = load16_fast<0>(rs, aw[i]);
+            dh[i] = load16_fast<AUX>(rs, ah[i]);
+            dt[i] = load16_fast<AUX>(rs, at[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            const int k = h * kHalf + i;
+            u32x4 v = dw[i], vh = dh[i], vt = dt[i];
+            if (__builtin_expect(straddles(aw[i], fb), 0)) v = load16(rs, aw[i], fb);
+            if (__builtin_expect(lh[i] != 0 && straddles(ah[i], fb), 0)) vh = load16(rs, ah[i], fb);
+            if (__builtin_expect(lt[i] != 0 && straddles(at[i], fb), 0)) vt = load16(rs, at[i], fb);
+            put_chunk(W, k * kWave + lane, v);
+            const uint32_t xh = sum8_lanes(lh[i] ? chunk_sum(vh, 0, (int)lh[i]) : 0u);
+            const uint32_t xt = sum8_lanes(lt[i] ? chunk_sum(vt, 0, (int)lt[i]) : 0u);
+            if (j == 0) {
+                W.first[(k * kWave + lane) >> 3] = xh;
+                W.last[(k * kWave + lane) >> 3] = xt;
+            }
+        }
+    }
+    wave_sync();
+    uint32_t wend, fend, he, tb;
+    edge_spans(fr.off, valid ? fr.len : 0u, wend, fend, he, tb);
+    return EdgeLines{true, W.first[lane] + W.last[lane], he, tb};
+}
+
 // ---- dword-granular LDS access for the parse ----
 // Frame byte x of this lane lives at LDS offset ph + x of its slot (ph = frame
 // offset & 15, the absolute 16-byte phase), so aligned LDS dwords are aligned in

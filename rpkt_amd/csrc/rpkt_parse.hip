@@ -91,6 +91,9 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
 // OPTS: also walk each frame's IPv4 and TCP options (rpkt_gpu_parse_options_batch) from
 // the header window the parse holds, between the parse and the L4 stream.
 // The tile of frames [p0, p0 + 64) of a batch, by one wave with its scratch W (p0 < n).
+#ifndef RPKT_EDGE_JOINT
+#define RPKT_EDGE_JOINT 1          // 0: the edge lines in their own pass after the window
+#endif
 // INWIN: every frame of the batch lies inside its header window (a strided batch of
 // short frames, window_fits), so the L4 sums are whole in LDS and step 3 (the edge lines
 // and the stream past the window) is compiled out.
@@ -107,29 +110,39 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, frames_bytes);
     const SpanSrc spans{offsets, stride, frame_len, frames_bytes, n};
 
-    // 1. header windows -> LDS (then, on long tiles, the edge lines: edge_lines_first)
+    // 1. header windows -> LDS; on long tiles with the edge lines (window_with_edges)
     const Frame fr = spans.get(i);
     const uint32_t wend = (fr.off & ~15u) + kWin, fend = fr.off + fr.len;
-    {
-        u32x4 d[kWinChunks];
-        uint32_t addr[kWinChunks];
-        // header-only batches read each frame line once: non-temporal window loads
-        // (config 2: 27.2 -> 26.1 us, profiles/r02_ablate_c2_v21.log); with the L4
-        // stream the window's lines are shared with the stream, and nt there costs
-        // +13-30 % (configs 3-5)
-        constexpr int kWinAux = (V == 21 || (!L4 && V != 45)) ? 2 : 0;
-        const uint32_t fix = window_issue<kWinAux>(rs, frames_bytes, fr, lane, d, addr);
-        window_commit(W, rs, frames_bytes, d, addr, fix, lane);
-    }
     EdgeLines X{false, 0u, 0u, 0u};
-    // tiles streaming more than 32 KB sum their frames' edge lines with the window
-    // (edge_lines_window; profiles/r02_edge_window: config 5 -1.2 % time and -9 % read
-    // traffic, configs 3 and 4 unchanged in time; every tile: config 4 +10 %)
-    if constexpr (L4 && !INWIN && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
-        X = edge_lines_window(rs, frames_bytes, W, lane, fr, valid,
-                              V == 40 ? 0u : V == 41 ? 16384u : V == 43 ? 65536u : kEdgeWindowBytes);
-    else if constexpr (L4 && V == 44)                  // the round-1 split: a pass after the window
-        X = edge_lines_first(rs, frames_bytes, W, lane, valid, wend, fend);
+    // header-only batches read each frame line once: non-temporal window loads
+    // (config 2: 27.2 -> 26.1 us, profiles/r02_ablate_c2_v21.log); with the L4 stream the
+    // window's lines are shared with the stream, and nt there costs +13-30 % (configs 3-5)
+    constexpr int kWinAux = (V == 21 || (!L4 && V != 45)) ? 2 : 0;
+    constexpr bool kJoint = L4 && !INWIN && RPKT_EDGE_JOINT && (V == 0 || V == 50) && kWinChunks == 8;
+    bool joint = false;
+    if constexpr (kJoint) {
+        // tiles streaming more than 32 KB sum their frames' edge lines with the window
+        // (profiles/r02_edge_window: config 5 -9 % read traffic), loaded together with it
+        const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
+        joint = wave_sum(span) > kEdgeWindowBytes;                    // wave-uniform
+    }
+    if (joint) {
+        if constexpr (kJoint) X = window_with_edges(rs, frames_bytes, W, lane, fr, valid);
+    } else {
+        {
+            u32x4 d[kWinChunks];
+            uint32_t addr[kWinChunks];
+            const uint32_t fix = window_issue<kWinAux>(rs, frames_bytes, fr, lane, d, addr);
+            window_commit(W, rs, frames_bytes, d, addr, fix, lane);
+        }
+        // (ablation variants: the edge lines in their own pass after the window, at other
+        // thresholds, or the round-1 split)
+        if constexpr (L4 && !INWIN && !kJoint && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
+            X = edge_lines_window(rs, frames_bytes, W, lane, fr, valid,
+                                  V == 40 ? 0u : V == 41 ? 16384u : V == 43 ? 65536u : kEdgeWindowBytes);
+        else if constexpr (L4 && V == 44)
+            X = edge_lines_first(rs, frames_bytes, W, lane, valid, wend, fend);
+    }
     wave_sync();
 
     // 2. lane-per-frame parse
