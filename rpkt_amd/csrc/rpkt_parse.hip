@@ -122,9 +122,13 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
     bool joint = false;
     if constexpr (kJoint) {
         // tiles streaming more than 32 KB sum their frames' edge lines with the window
-        // (profiles/r02_edge_window: config 5 -9 % read traffic), loaded together with it
+        // (profiles/r02_edge_window: config 5 -9 % read traffic); beyond 64 KB (1500-B
+        // frames) loaded together with it: config 3 reads 1.042x -> 1.000x its frame
+        // bytes, 269.0 -> 265.7 us, config 11 279.6 -> 275.0 us; config 5's 40-60 KB
+        // tiles read 3.7 % less that way too but ran 2.3 % slower, so they keep the
+        // separate edge pass (profiles/r04_wpb/ab_joint_*.jsonl)
         const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
-        joint = wave_sum(span) > kEdgeWindowBytes;                    // wave-uniform
+        joint = wave_sum(span) > kSplitStreamBytes;                   // wave-uniform
     }
     if (joint) {
         if constexpr (kJoint) X = window_with_edges(rs, frames_bytes, W, lane, fr, valid);
@@ -137,7 +141,7 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
         }
         // (ablation variants: the edge lines in their own pass after the window, at other
         // thresholds, or the round-1 split)
-        if constexpr (L4 && !INWIN && !kJoint && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
+        if constexpr (L4 && !INWIN && V != 1 && V != 23 && V != 24 && V != 25 && V != 44)
             X = edge_lines_window(rs, frames_bytes, W, lane, fr, valid,
                                   V == 40 ? 0u : V == 41 ? 16384u : V == 43 ? 65536u : kEdgeWindowBytes);
         else if constexpr (L4 && V == 44)
