@@ -124,11 +124,13 @@ __device__ __forceinline__ void parse_tile(WaveScratch& W, const uint8_t* opt_ru
         // tiles streaming more than 32 KB sum their frames' edge lines with the window
         // (profiles/r02_edge_window: config 5 -9 % read traffic); beyond 64 KB (1500-B
         // frames) loaded together with it: config 3 reads 1.042x -> 1.000x its frame
-        // bytes, 269.0 -> 265.7 us, config 11 279.6 -> 275.0 us; config 5's 40-60 KB
-        // tiles read 3.7 % less that way too but ran 2.3 % slower, so they keep the
-        // separate edge pass (profiles/r04_wpb/ab_joint_*.jsonl)
+        // bytes, 269.0 -> 265.7 us, config 11 279.6 -> 275.0 us.  The parse of config 5's
+        // 40-60 KB tiles read 3.7 % less that way too but ran 2.3 % slower, so it keeps
+        // the separate edge pass; its fused option walks (4-wave blocks) ran 2.7 % faster
+        // and take the joint loads from 32 KB (profiles/r04_wpb/ab_joint_*.jsonl)
+        constexpr uint32_t kJointMin = OPTS ? kEdgeWindowBytes : kSplitStreamBytes;
         const uint32_t span = (valid && fend > wend) ? fend - wend : 0u;
-        joint = wave_sum(span) > kSplitStreamBytes;                   // wave-uniform
+        joint = wave_sum(span) > kJointMin;                           // wave-uniform
     }
     if (joint) {
         if constexpr (kJoint) X = window_with_edges(rs, frames_bytes, W, lane, fr, valid);
