@@ -1275,9 +1275,28 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_compact_w64(
                   (rpkt_rec_t*)recs_dev, (uint64_t*)flow_ev_dev, n_buckets,
                   (rpkt_opts_t*)nullptr);
 }
+// 80-B records with the L4 sum (RPKT_PARSE_W64_FULL): the record stage keeps the
+// window area at 5376 B, so a wave needs 6.5 KB of LDS instead of 9.7 KB and the
+// in-window L4 instantiation (68 VGPRs) runs 6 waves per SIMD instead of 4
+__attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_l4_w64(
+    const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs_dev, rpkt_flow_ev_t* flow_ev_dev,
+    uint32_t n_buckets, void* stream) {
+    const uint32_t flen = b->frame_len ? b->frame_len : b->stride;
+    const uint32_t per_block = kWave * kParseWPB;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    return launch(parse_kernel<true, 0, false, false, kParseWPB, true>, dim3(grid),
+                  dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
+                  recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
+}
 #else
 int rpkt_gpu_parse_batch_compact_w64(const rpkt_batch_t*, uint32_t, rpkt_rec16_t*,
                                      rpkt_flow_ev_t*, uint32_t, void*);
+int rpkt_gpu_parse_batch_l4_w64(const rpkt_batch_t*, uint32_t, rpkt_rec_t*, rpkt_flow_ev_t*,
+                                uint32_t, void*);
+#ifndef RPKT_PARSE_W64_FULL
+#define RPKT_PARSE_W64_FULL 1
+#endif
 int rpkt_gpu_parse_ring_compact_w64(const rpkt_ring_slot_t*, uint32_t, uint32_t, uint32_t, void*);
 
 // every frame of a strided batch inside a 64-B window from its 16-B boundary
@@ -1316,6 +1335,8 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
         if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
     }
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    if (RPKT_PARSE_W64_ON && RPKT_PARSE_W64_FULL && (flags & RPKT_F_L4_SUM) && parse_w64_fits(b, flen))
+        return rpkt_gpu_parse_batch_l4_w64(b, flags, recs_dev, flow_ev_dev, n_buckets, stream);
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
     auto k = !(flags & RPKT_F_L4_SUM)     ? parse_kernel<false, 0, false, false, kParseWPB>
