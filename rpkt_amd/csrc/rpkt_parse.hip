@@ -1284,8 +1284,9 @@ __attribute__((visibility("hidden"))) int rpkt_gpu_parse_batch_l4_w64(
     const uint32_t flen = b->frame_len ? b->frame_len : b->stride;
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
-    return launch(parse_kernel<true, 0, false, false, kParseWPB, true>, dim3(grid),
-                  dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
+    auto k = (flags & RPKT_F_L4_SUM) ? parse_kernel<true, 0, false, false, kParseWPB, true>
+                                     : parse_kernel<false, 0, false, false, kParseWPB>;
+    return launch(k, dim3(grid), dim3(per_block), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags,
                   recs_dev, (uint64_t*)flow_ev_dev, n_buckets, (rpkt_opts_t*)nullptr);
 }
@@ -1335,7 +1336,8 @@ int rpkt_gpu_parse_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* recs
         if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
     }
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
-    if (RPKT_PARSE_W64_ON && RPKT_PARSE_W64_FULL && (flags & RPKT_F_L4_SUM) && parse_w64_fits(b, flen))
+    if (RPKT_PARSE_W64_ON && RPKT_PARSE_W64_FULL && ((flags & RPKT_F_L4_SUM) || RPKT_PARSE_W64_FULL > 1) &&
+        parse_w64_fits(b, flen))
         return rpkt_gpu_parse_batch_l4_w64(b, flags, recs_dev, flow_ev_dev, n_buckets, stream);
     const uint32_t per_block = kWave * kParseWPB;
     const uint32_t grid = (b->n + per_block - 1) / per_block;
