@@ -71,3 +71,26 @@ def test_full_profile_keeps_single_legs_of_unchanged_units(tmp_path):
     fake_profile(tmp_path / "full3", build_str(tx="t2", walks="w2"), KERNELS.values(), 1.0, 1.0)
     run(tmp_path / "full3", "tx", out)
     assert set(json.loads(out.read_text())["legs"]) == set(KERNELS)
+
+
+def test_read_request_sizes(tmp_path):
+    """The optional rdreq pass (scripts/profile.sh): the exact read bytes are 32 n32 +
+    64 n64 + 128 n128 per launch (warm-up launches skipped), reported beside
+    FETCH_SIZE x2 and their ratio, per TX/walk leg."""
+    out = tmp_path / "traffic_tx.json"
+    d = tmp_path / "full"
+    fake_profile(d, build_str(), KERNELS.values(), 100.0, 50.0)
+    with open(os.path.join(d, "rdreq_counter_collection.csv"), "w", newline="") as fh:
+        w = csv.DictWriter(fh, ["Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for k in KERNELS.values():
+            for _ in range(10):
+                for name, v in (("TCC_EA0_RDREQ_32B_sum", 0.0), ("TCC_EA0_RDREQ_64B_sum", 2.0),
+                                ("TCC_EA0_RDREQ_128B_sum", 1600.0), ("TCC_EA0_RDREQ_sum", 1602.0)):
+                    w.writerow({"Kernel_Name": k + "(args)", "Counter_Name": name,
+                                "Counter_Value": v})
+    run(d, "tx", out)
+    leg = json.loads(out.read_text())["legs"]["layers9"]
+    assert leg["read_bytes_by_request_size"] == 2 * 64 + 1600 * 128
+    assert abs(leg["fetch_x2_over_by_size"] - 100.0 * 2048 / (2 * 64 + 1600 * 128)) < 1e-12
+    assert leg["rdreq"]["TCC_EA0_RDREQ_sum"] == 1602.0
