@@ -971,27 +971,147 @@ def run_tx(cfg, mode, args, rank, world):
                      "sources, swap + ttl-1 + MACs + checksum update)")}
 
 
+LINE_MAX = 8000           # the driver keeps an 8,000-char tail of stdout: the line fits it
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "gb_per_s", "all_cores_mpps",
+            "all_cores_gb_per_s", "all_cores_threads", "gpu_parity_on_sample", "cpu_model")
+FLOW_KEYS = ("flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified", "flow_reduce_error",
+             "flow_pkts_total", "flow_pkts_expected")
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def leg_summary(v):
+    """One extra leg in the stdout line: its kernel time, step time, roofline fraction and
+    PMC traffic over algorithmic bytes (the rest of the leg is in the detail file)."""
+    if "roofline" in v:
+        rf = v["roofline"]
+        t, a = rf.get("traffic"), rf.get("alg_bytes_per_launch")
+        s = {"kernel_ms": _r(v.get("kernel_ms"), 5), "ms_per_step": _r(v.get("ms_per_step"), 5),
+             "frac": rf.get("frac"), "traffic_ratio": round(t / a, 4) if t and a else None}
+        for k in ("mpps", "flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified"):
+            if k in v:
+                s[k] = _r(v[k], 3)
+        return s
+    if "ns_per_pkt" in v:                                          # config 1 (host CPU)
+        return {"ns_per_pkt": v["ns_per_pkt"], "mpps": v["mpps"], "cores": v["cores"]}
+    # nested legs (host_inclusive, rx_graph): the rate of every sub-leg, checks kept
+    out = {}
+    for k, sub in v.items():
+        if isinstance(sub, dict):
+            out[k] = (round(sub["mpps"], 1) if "mpps" in sub else
+                      {kk: (round(vv["mpps"], 1) if isinstance(vv, dict) and "mpps" in vv else vv)
+                       for kk, vv in sub.items()})
+            if isinstance(sub, dict) and sub.get("records_checked") is False:
+                out[k + "_records_checked"] = False
+        else:
+            out[k] = _r(sub)
+    return out
+
+
+def headline_line(main_res, extra, args, world, engine_build, detail_path):
+    """The one JSON line rank 0 prints: the driver's contract keys, the main leg's
+    roofline and CPU baseline (top-level scalars), the flow-reduce fields, and per extra
+    leg only its times and fractions.  Always < LINE_MAX bytes: when a leg set would not
+    fit, the per-leg summaries shrink to the roofline fraction alone."""
+    fb = {2: 64, 3: 1500, 7: 8000, 10: 64, 11: 1500}.get(args.config)
+    rf = dict(main_res["roofline"])
+    rf.pop("traffic_source", None)
+    cpu = main_res.get("cpu_baseline")
+    line = {
+        "metric": METRIC,
+        "value": round(main_res["mpps"], 2),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(main_res["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": main_res["scaling"],
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded generator, rpkt-dpdk loopback_tx frame shapes)",
+        "config": {"workload": WORKLOAD[args.config], "frames_per_rank":
+                   main_res["frames_per_rank"], "frame_bytes": fb,
+                   "layout": main_res["layout"], "checksums": main_res["flags"],
+                   "parallelism": "replicas x%d (independent batches, no collective)" % world
+                   if args.config != 4 else "shard x%d + RCCL all-reduce" % world,
+                   "dist_backend": args.dist_backend if world > 1 else None},
+        "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
+        "kernel_ms": round(main_res["kernel_ms"], 5),
+        "engine_build": engine_build,
+        "roofline": rf,
+        "cpu_baseline": {k: cpu[k] for k in CPU_KEYS if k in cpu} if cpu else None,
+        "detail": detail_path,
+    }
+    for k in FLOW_KEYS:
+        if k in main_res:
+            line[k] = main_res[k]
+    if "copy_ceiling" in main_res:
+        line["copy_ceiling_gb_per_s"] = {k: v.get("gb_per_s") for k, v in
+                                         main_res["copy_ceiling"].items() if isinstance(v, dict)}
+    # flow-reduce fields of an extra config-4 leg at the top level too (the N-rank check)
+    for k in FLOW_KEYS:
+        if k not in line and "config4" in extra and k in extra["config4"]:
+            line[k] = extra["config4"][k]
+    line["extra"] = {k: leg_summary(v) for k, v in extra.items()}
+    if len(json.dumps(line)) >= LINE_MAX:
+        line["extra"] = {k: (s.get("frac") if "frac" in s else s.get("mpps"))
+                         for k, s in line["extra"].items()}
+    if len(json.dumps(line)) >= LINE_MAX:
+        line["extra"] = {"omitted": "see detail"}
+    return line
+
+
+def write_detail(path, main_res, extra, args, world, engine_build):
+    """Every leg's full result (what it measured, layouts, line floors, CPU samples) to a
+    side file; the stdout line names it."""
+    full = {"metric": METRIC, "n_gpus": world, "argv": sys.argv[1:], "engine_build": engine_build,
+            "main": main_res, "extra": extra}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(path, "w") as fh:
+        json.dump(full, fh, indent=1, default=lambda o: _r(float(o)) if hasattr(o, "__float__")
+                  else str(o))
+
+
+# legs run by default at N = 1, and at N > 1 unless --all-legs (the N-rank job stays short:
+# the headline, config 4's sharded parse + counter reduce, and the strong-scaling legs)
+LEG_DEFAULTS = {"also": ("3,4,5,7,10,11", "4"),
+                "tx": ("build2,build3,forward2,opts5,optsc5,layers9,fields9", ""),
+                "compact": ("2,3", ""), "strong": ("2,3", "2,3"), "opts": ("5", ""),
+                "ring": ("2,10", "")}
+
+
+def resolve_legs(args, world):
+    for k, (one, many) in LEG_DEFAULTS.items():
+        if getattr(args, k) is None:
+            setattr(args, k, one if world == 1 or args.all_legs else many)
+    return args
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 7, 10, 11])
-    ap.add_argument("--also", default="3,4,5,7,10,11",
-                    help="extra configs reported under 'extra'")
+    ap.add_argument("--also", default=None,
+                    help="extra configs reported under 'extra' (default 3,4,5,7,10,11; 4 at N>1)")
     ap.add_argument("--frames", type=int, default=0, help="override frames per batch")
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="all-cores CPU leg threads (0 = every usable host thread)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tx", default="build2,build3,forward2,opts5,optsc5,layers9,fields9",
-                    help="legs beyond the parse reported under 'extra' (build<cfg>, "
+    ap.add_argument("--tx", default=None,
+                    help="legs beyond the parse reported under 'extra' (default "
+                         "build2,build3,forward2,opts5,optsc5,layers9,fields9; none at N>1) (build<cfg>, "
                          "forward<cfg>, opts<cfg>, optsc<cfg> (compact records), layers9, "
                          "fields9)")
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
-    ap.add_argument("--reduce-comm", default="own", choices=["own", "auto", "torch"],
+    ap.add_argument("--reduce-comm", default="auto", choices=["own", "auto", "torch"],
                     help="flow-counter reduce: rpkt_gpu_flow_reduce on the library's own RCCL "
                          "communicator (own), on torch's (auto), or torch's all_reduce (torch)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -1001,7 +1121,7 @@ def main():
                     help="record size of the main leg (profiling the compact kernel alone)")
     ap.add_argument("--main-opts", action="store_true",
                     help="main leg as the fused parse + option walks (profiling it alone)")
-    ap.add_argument("--compact", default="2,3",
+    ap.add_argument("--compact", default=None,
                     help="configs also timed with 16-B compact records (extra.config<N>_compact)")
     ap.add_argument("--host", default="2,3",
                     help="configs also timed host-inclusive at N=1 (pinned H2D frames -> parse "
@@ -1009,15 +1129,20 @@ def main():
     ap.add_argument("--rx-graph", default="16384x64,65536x16",
                     help="receive loops of small config-2 batches, FRAMESxSLOTS, timed eager "
                          "and as a replayed hipGraph at N=1 (rpkt_amd.graphs): extra.rx_graph")
-    ap.add_argument("--strong", default="2,3",
+    ap.add_argument("--strong", default=None,
                     help="configs also timed as one batch split over the ranks "
                          "(extra.config<N>_strong)")
-    ap.add_argument("--ring", default="2",
+    ap.add_argument("--ring", default=None,
                     help="configs also timed as 8 full batches per rpkt_gpu_parse_ring launch "
+                         "(default 2,10; none at N>1) "
                          "(extra.config<N>_ring8[_compact])")
-    ap.add_argument("--opts", default="5",
+    ap.add_argument("--opts", default=None,
                     help="configs also timed as the fused parse + option walks "
                          "(extra.config<N>_opts, extra.config<N>_opts_compact)")
+    ap.add_argument("--all-legs", action="store_true",
+                    help="at N>1, run every N=1 default leg too (longer job)")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="side file with every leg's full result (the stdout line names it)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -1053,6 +1178,7 @@ def main():
             print("[bench] error: world size %d != --gpus %d" % (dist.get_world_size(),
                                                                   args.gpus), file=sys.stderr)
             sys.exit(3)
+    resolve_legs(args, world)
     want_cpu = (not args.no_cpu) and world == 1
     if not args.cpu_threads:
         args.cpu_threads = usable_cpus()
@@ -1084,39 +1210,13 @@ def main():
         extra["config1"] = run_config1(args)
 
     if rank == 0:
-        fb = {2: 64, 3: 1500, 7: 8000, 10: 64, 11: 1500}.get(args.config)
-        line = {
-            "metric": METRIC,
-            "value": round(main_res["mpps"], 2),
-            "unit": "Mpps",
-            "n_gpus": dist.get_world_size() if world > 1 else 1,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(main_res["ms_per_step"], 4),
-            "higher_is_better": True,
-            "scaling": main_res["scaling"],
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (seeded generator, rpkt-dpdk loopback_tx frame shapes)",
-            "config": {"workload": WORKLOAD[args.config], "frames_per_rank":
-                       main_res["frames_per_rank"], "frame_bytes": fb,
-                       "layout": main_res["layout"], "checksums": main_res["flags"],
-                       "parallelism": "replicas x%d (independent batches, no collective)" % world
-                       if args.config != 4 else "shard x%d + RCCL all-reduce" % world,
-                       "dist_backend": args.dist_backend if world > 1 else None},
-            "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
-            "kernel_ms": round(main_res["kernel_ms"], 5),
-            "warmup_launches": main_res["warmup_launches"],
-            "engine_build": engine.lib().rpkt_gpu_build_info().decode(),
-            "roofline": main_res["roofline"],
-            "cpu_baseline": main_res.get("cpu_baseline"),
-            "extra": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
-                          for kk, vv in v.items()} for k, v in extra.items()},
-        }
-        for k in ("flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified", "flow_reduce_error",
-                  "flow_pkts_total", "flow_pkts_expected", "copy_ceiling"):
-            if k in main_res:
-                line[k] = main_res[k]
+        build = engine.lib().rpkt_gpu_build_info().decode()
+        detail = os.path.relpath(args.detail, ROOT)
+        try:
+            write_detail(args.detail, main_res, extra, args, world, build)
+        except OSError as e:
+            detail = "not written: %s" % e
+        line = headline_line(main_res, extra, args, world, build, detail)
         print(json.dumps(line), flush=True)
     # a counter sum that is wrong (not merely taken by the fallback path) fails the run
     bad_counters = any(r.get("flow_reduce_verified") is False or

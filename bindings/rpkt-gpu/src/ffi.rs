@@ -272,6 +272,12 @@ extern "C" {
     pub fn rpkt_gpu_comm_init(comm_out: *mut *mut c_void, world: c_int, id: *const u8,
                               rank: c_int) -> c_int;
     pub fn rpkt_gpu_comm_destroy(comm: *mut c_void) -> c_int;
+    /// rpkt_gpu_comm_init with a deadline: non-blocking init polled for `timeout_ms`,
+    /// aborted (RPKT_E_COLL, last_coll_error 7) when not every rank joins in time.
+    pub fn rpkt_gpu_comm_init_timeout(comm_out: *mut *mut c_void, world: c_int, id: *const u8,
+                                      rank: c_int, timeout_ms: c_int) -> c_int;
+    /// ncclCommAbort: release a communicator without waiting for its peers.
+    pub fn rpkt_gpu_comm_abort(comm: *mut c_void) -> c_int;
 
     pub fn rpkt_gpu_checksum_ranges(buf_dev: *const u8, buf_bytes: u64, ranges_dev: *const u32,
                                     n: u32, out_dev: *mut u16, stream: *mut c_void) -> c_int;

@@ -318,6 +318,16 @@ int rpkt_gpu_coll_version(void);
 int rpkt_gpu_coll_unique_id(uint8_t* id_out);
 int rpkt_gpu_comm_init(void** comm_out, int world, const uint8_t* id, int rank);
 int rpkt_gpu_comm_destroy(void* comm);
+/* rpkt_gpu_comm_init with a deadline (timeout_ms <= 0: blocking, as rpkt_gpu_comm_init):
+ * a non-blocking ncclCommInitRankConfig polled with ncclCommGetAsyncError.  When not
+ * every rank joins within timeout_ms (a peer failed before its init) or the init fails,
+ * the half-made communicator is aborted and RPKT_E_COLL returned
+ * (rpkt_gpu_last_coll_error() = 7, ncclInProgress, on a timeout), so no rank is left
+ * blocked and the group can agree on a fallback.  rpkt_gpu_comm_abort (ncclCommAbort)
+ * releases a communicator without waiting for its peers. */
+int rpkt_gpu_comm_init_timeout(void** comm_out, int world, const uint8_t* id, int rank,
+                               int timeout_ms);
+int rpkt_gpu_comm_abort(void* comm);
 
 /* Batched checksum::from_slice over byte ranges of a device buffer:
  * out_dev[i] = from_slice(buf[start_i .. start_i + len_i]) for

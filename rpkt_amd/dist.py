@@ -25,6 +25,9 @@ import torch.distributed as dist
 last_reduce_path = None      # "rccl_own" | "rccl" | "torch" | "gloo" | "local" after reduce_counters
 _own_comms = {}              # process group -> the library's own ncclComm_t (as int)
 last_reduce_error = None     # why the group did not take the C ABI path (None if it did)
+last_exchange_error = None   # on rank 0: why make_id() failed in the last exchange_id
+# how long rpkt_gpu_comm_init_timeout waits for every rank to join before it aborts
+COMM_INIT_TIMEOUT_MS = 60000
 
 
 def shard_range(n, rank, world):
@@ -46,18 +49,21 @@ def agree(ok, group=None):
 def exchange_id(make_id, group=None, nbytes=128):
     """Rank 0 of the group calls make_id() (the RCCL unique id, `nbytes` bytes) and the
     group broadcasts it: every rank returns the same bytes, or None on every rank when
-    rank 0 could not make one (a flag travels with the id, so no rank waits alone)."""
+    rank 0 could not make one (a flag travels with the id, so no rank waits alone).  Rank
+    0 keeps the reason in `last_exchange_error`."""
+    global last_exchange_error
+    last_exchange_error = None
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
     buf = torch.zeros(1 + nbytes, dtype=torch.uint8)
     if dist.get_rank(group) == 0:
         try:
             uid = bytes(make_id())
             if len(uid) != nbytes:
-                raise ValueError("id of %d bytes" % len(uid))
+                raise ValueError("id of %d bytes, want %d" % (len(uid), nbytes))
             buf[0] = 1
             buf[1:] = torch.tensor(list(uid), dtype=torch.uint8)
-        except Exception:                        # the flag stays 0: every rank gets None
-            pass
+        except Exception as e:                   # the flag stays 0: every rank gets None
+            last_exchange_error = "%s: %s" % (type(e).__name__, e)
     buf = buf.to(dev)
     src = dist.get_global_rank(group, 0) if group is not None else 0
     dist.broadcast(buf, src=src, group=group)
@@ -65,16 +71,23 @@ def exchange_id(make_id, group=None, nbytes=128):
     return bytes(buf[1:].tolist()) if int(buf[0]) else None
 
 
-def own_comm(group=None):
+def own_comm(group=None, timeout_ms=None, _engine=None):
     """(comm, None): the library's own RCCL communicator over the group's ranks (made on
     first use, then cached), or (None, reason) on every rank when the group cannot make
     one.  Every rank must first be able to call RCCL through the engine (agreed), then
-    rank 0's id is broadcast and all ranks join it (rpkt_gpu_comm_init, collective)."""
+    rank 0's id is broadcast and all ranks join it with rpkt_gpu_comm_init_timeout: a
+    rank whose peer never joins (it failed before its init) gets its half-made
+    communicator aborted after `timeout_ms` instead of blocking, and the group then
+    agrees whether every rank holds a communicator, so either all ranks use it or none
+    does (a rank that made one aborts it).  `_engine` replaces the engine module in CPU
+    tests."""
     key = group if group is not None else dist.group.WORLD
     if key in _own_comms:
         return _own_comms[key], None
+    engine = _engine
     try:
-        from . import engine
+        if engine is None:
+            from . import engine
         can = engine.lib().rpkt_gpu_coll_version() > 0
         why = None if can else "RCCL not loadable by the engine"
     except Exception as e:                       # no engine on this rank
@@ -83,9 +96,21 @@ def own_comm(group=None):
         return None, why or "another rank cannot load RCCL"
     uid = exchange_id(engine.coll_unique_id, group, engine.COLL_ID_BYTES)
     if uid is None:
-        return None, "rank 0 could not make an RCCL unique id"
-    # collective from here: every rank joins, a failure raises (the others are inside)
-    comm = engine.comm_init(dist.get_world_size(group), uid, dist.get_rank(group))
+        return None, "rank 0 could not make an RCCL unique id%s" % (
+            ": " + last_exchange_error if last_exchange_error else "")
+    comm, why = None, None
+    try:
+        comm = engine.comm_init_timeout(dist.get_world_size(group), uid, dist.get_rank(group),
+                                        COMM_INIT_TIMEOUT_MS if timeout_ms is None else timeout_ms)
+    except Exception as e:                       # timed out, or the init failed
+        why = "comm init on rank %d: %s: %s" % (dist.get_rank(group), type(e).__name__, e)
+    if not agree(comm is not None, group):
+        if comm is not None:                     # the group gives it up: no collective on it
+            try:
+                engine.comm_abort(comm)
+            except Exception:
+                pass
+        return None, why or "another rank's rpkt_gpu_comm_init_timeout failed"
     _own_comms[key] = comm
     return comm, None
 

@@ -59,7 +59,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_batch_compact", "rpkt_gpu_options_batch_compact",
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
            "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact", "rpkt_gpu_coll_unique_id",
-           "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy"]
+           "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy", "rpkt_gpu_comm_init_timeout",
+           "rpkt_gpu_comm_abort"]
 COLL_ID_BYTES = 128
 
 _lib = None
@@ -151,6 +152,10 @@ def lib():
         L.rpkt_gpu_comm_init.restype = ctypes.c_int
         L.rpkt_gpu_comm_destroy.argtypes = [ctypes.c_void_p]
         L.rpkt_gpu_comm_destroy.restype = ctypes.c_int
+        L.rpkt_gpu_comm_init_timeout.argtypes = L.rpkt_gpu_comm_init.argtypes + [ctypes.c_int]
+        L.rpkt_gpu_comm_init_timeout.restype = ctypes.c_int
+        L.rpkt_gpu_comm_abort.argtypes = [ctypes.c_void_p]
+        L.rpkt_gpu_comm_abort.restype = ctypes.c_int
         L.rpkt_flow_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16,
                                      ctypes.c_uint16, ctypes.c_uint8]
         L.rpkt_flow_hash.restype = ctypes.c_uint32
@@ -373,8 +378,28 @@ def comm_init(world, uid, rank):
     return int(comm.value)
 
 
+def comm_init_timeout(world, uid, rank, timeout_ms):
+    """rpkt_gpu_comm_init_timeout: the same join, aborted after `timeout_ms` when not every
+    rank arrives (RpktError; last_coll_error() == 7 on a timeout)."""
+    if len(uid) != COLL_ID_BYTES:
+        raise RpktError("comm_init: the id must be %d bytes" % COLL_ID_BYTES)
+    buf = (ctypes.c_uint8 * COLL_ID_BYTES).from_buffer_copy(uid)
+    comm = ctypes.c_void_p()
+    rc = lib().rpkt_gpu_comm_init_timeout(ctypes.byref(comm), world, buf, rank, int(timeout_ms))
+    _check(rc, "rpkt_gpu_comm_init_timeout")
+    return int(comm.value)
+
+
+def last_coll_error():
+    return int(lib().rpkt_gpu_last_coll_error())
+
+
 def comm_destroy(comm):
     _check(lib().rpkt_gpu_comm_destroy(ctypes.c_void_p(int(comm))), "rpkt_gpu_comm_destroy")
+
+
+def comm_abort(comm):
+    _check(lib().rpkt_gpu_comm_abort(ctypes.c_void_p(int(comm))), "rpkt_gpu_comm_abort")
 
 
 def checksum_ranges(buf, ranges, out=None, stream=None):

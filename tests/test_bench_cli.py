@@ -36,8 +36,9 @@ def test_tx_leg_names():
         bench.tx_legs("nope2")
     with pytest.raises(SystemExit):
         bench.tx_legs("opts")
-    ap_default = [a for a in open(bench.__file__).read().split("\n") if '"--tx", default=' in a][0]
-    bench.tx_legs(ap_default.split('default="')[1].split('"')[0])
+    for one, many in [bench.LEG_DEFAULTS["tx"]]:
+        bench.tx_legs(one)
+        bench.tx_legs(many)
 
 
 def test_line_floor_matches_brute_force():
@@ -58,3 +59,73 @@ def test_line_floor_matches_brute_force():
         assert bench.line_floor(s, e) == 128 * len(lines)
     assert bench.line_floor([], []) == 0
     assert bench.line_floor([127], [129]) == 256 and bench.line_floor([128], [256]) == 128
+
+
+def _r04_legs():
+    """main_res / extra rebuilt from round 4's real 20-KB line (every leg populated)."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "r04_bench_final.json")) as fh:
+        L = json.load(fh)
+    main = {"mpps": L["value"], "ms_per_step": L["ms_per_step"], "scaling": L["scaling"],
+            "frames_per_rank": L["config"]["frames_per_rank"], "layout": L["config"]["layout"],
+            "flags": L["config"]["checksums"], "frame_gb_per_s": L["frame_gb_per_s"],
+            "kernel_ms": L["kernel_ms"], "roofline": L["roofline"],
+            "cpu_baseline": L["cpu_baseline"], "copy_ceiling": L["copy_ceiling"]}
+    return main, dict(L["extra"])
+
+
+class _Args:
+    config, steps, warmup, dist_backend = 2, 20, 5, "nccl"
+
+
+def test_headline_line_fits_the_driver_tail():
+    """The stdout line built from a fully populated leg set (round 4's, whose 20-KB line
+    the driver could not parse, plus 20 more synthetic legs) stays under 8,000 bytes and
+    keeps the contract keys, the roofline and the CPU baseline's all-cores scalars."""
+    import copy
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    main, extra = _r04_legs()
+    line = bench.headline_line(main, extra, _Args, 1, "x" * 400, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) < 8000, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "config", "roofline",
+              "cpu_baseline", "detail"):
+        assert k in line, k
+    assert line["roofline"]["frac"] == main["roofline"]["frac"]
+    for k in ("value", "cores", "kind", "sample", "all_cores_mpps", "all_cores_threads"):
+        assert k in line["cpu_baseline"], k
+    assert set(line["extra"]) == set(extra)
+    assert line["extra"]["config3"]["frac"] == extra["config3"]["roofline"]["frac"]
+    assert "what" not in s
+    assert line["extra"]["config4"]["flow_reduce_via"] == extra["config4"]["flow_reduce_via"]
+    # twice the legs still fits (summaries shrink to the fraction alone)
+    more = dict(extra)
+    for k, v in extra.items():
+        more[k + "_again"] = copy.deepcopy(v)
+    line2 = bench.headline_line(main, more, _Args, 8, "x" * 400, "gpurun_out/bench_detail.json")
+    assert len(json.dumps(line2)) < 8000
+    assert line2["n_gpus"] == 8
+
+
+def test_n_rank_default_leg_set():
+    """At N > 1 the default job is the headline, config 4 (shards + counter reduce) and the
+    strong legs; --all-legs restores the N = 1 set; explicit flags win."""
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def ns(**kw):
+        d = {k: None for k in bench.LEG_DEFAULTS}
+        d.update(all_legs=False)
+        d.update(kw)
+        return argparse.Namespace(**d)
+    a = bench.resolve_legs(ns(), 8)
+    assert (a.also, a.tx, a.compact, a.strong, a.opts, a.ring) == ("4", "", "", "2,3", "", "")
+    one = bench.resolve_legs(ns(), 1)
+    assert one.tx.startswith("build2") and "4" in one.also.split(",")
+    allg = bench.resolve_legs(ns(all_legs=True), 8)
+    assert allg.tx == one.tx and allg.also == one.also
+    assert bench.resolve_legs(ns(tx="layers9"), 8).tx == "layers9"

@@ -119,3 +119,78 @@ def test_own_communicator_id_exchange(tmp_path, world, fail):
     mp.spawn(_id_worker, args=(world, _free_port(), fail, out), nprocs=world, join=True)
     got = {open("%s.%d" % (out, r), "rb").read() for r in range(world)}
     assert got == {b"NONE" if fail else bytes(range(128))}
+
+
+class _StubLib:
+    def rpkt_gpu_coll_version(self):
+        return 22700
+
+
+class _StubEngine:
+    """Stands in for rpkt_amd.engine in own_comm: rank `fail_rank`'s comm init fails (as a
+    peer that never joins makes the others' rpkt_gpu_comm_init_timeout time out), or rank
+    0's id cannot be made."""
+    COLL_ID_BYTES = 128
+
+    def __init__(self, rank, fail_rank, fail_id, log):
+        self.rank, self.fail_rank, self.fail_id, self.log = rank, fail_rank, fail_id, log
+
+    def lib(self):
+        return _StubLib()
+
+    def coll_unique_id(self):
+        if self.fail_id:
+            raise RuntimeError("rpkt_gpu_coll_unique_id failed: RCCL error (ncclResult 2)")
+        return bytes(range(128))
+
+    def comm_init_timeout(self, world, uid, rank, timeout_ms):
+        assert uid == bytes(range(128)) and timeout_ms > 0
+        if rank == self.fail_rank:
+            raise RuntimeError("rpkt_gpu_comm_init_timeout failed: RCCL error (ncclResult 7)")
+        return 0x1000 + rank
+
+    def comm_abort(self, comm):
+        self.log.append(("abort", comm))
+
+
+def _own_worker(rank, world, port, fail_rank, fail_id, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rpkt_amd import dist as rd
+    log = []
+    comm, why = rd.own_comm(timeout_ms=5000,
+                            _engine=_StubEngine(rank, fail_rank, fail_id, log))
+    with open("%s.%d" % (out, rank), "w") as fh:
+        fh.write("%s|%s|%s" % (comm, why, ",".join("%s:%s" % x for x in log)))
+    rd._own_comms.clear()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,fail_id", [(2, -1, False), (2, 1, False),
+                                                     (3, 0, False), (3, 2, False),
+                                                     (2, -1, True)])
+def test_own_comm_init_failure_is_agreed(tmp_path, world, fail_rank, fail_id):
+    """One rank's communicator init fails (or rank 0 cannot make the id): own_comm returns
+    (None, reason) on EVERY rank, the ranks whose init succeeded abort their half of the
+    communicator, and rank 0's reason names the cause; with no failure every rank keeps
+    its communicator."""
+    out = str(tmp_path / "own")
+    mp.spawn(_own_worker, args=(world, _free_port(), fail_rank, fail_id, out), nprocs=world,
+             join=True)
+    res = [open("%s.%d" % (out, r)).read().split("|") for r in range(world)]
+    if fail_rank < 0 and not fail_id:
+        assert [c for c, _, _ in res] == [str(0x1000 + r) for r in range(world)]
+        assert all(w == "None" and a == "" for _, w, a in res)
+        return
+    assert all(c == "None" for c, _, _ in res)
+    for r, (_, why, aborted) in enumerate(res):
+        assert why != "None"
+        if fail_id:
+            assert aborted == ""
+            if r == 0:
+                assert "ncclResult 2" in why
+        elif r == fail_rank:
+            assert "ncclResult 7" in why and aborted == ""
+        else:
+            assert aborted == "abort:%d" % (0x1000 + r)

@@ -72,21 +72,31 @@ def test_ranks_hip_flow_counters_equal_whole_batch(tmp_path, world):
     assert np.array_equal(got.reshape(-1, 4), want)
 
 
-def test_bench_launches_two_ranks():
-    """bench.py --gpus 2 starts its own two ranks (no torchrun), each parses its shard of
-    config 4 and the counter sum covers every frame of every launch of every rank."""
+def test_bench_launches_two_ranks(tmp_path):
+    """bench.py --gpus 2 starts its own two ranks (no torchrun) and runs the N-rank default
+    leg set (the headline, config 4's shards + counter reduce, the strong legs): the
+    counter sum covers every frame of every launch of every rank and is verified against
+    torch's sum, and rank 0's one stdout line parses and fits the driver's 8,000-char
+    tail."""
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
+    detail = str(tmp_path / "detail.json")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
-                        "--dist-backend", "gloo", "--config", "4", "--also", "", "--tx", "",
-                        "--no-cpu", "--frames", "400000", "--steps", "3", "--warmup", "1",
-                        "--min-warmup-s", "0"], capture_output=True, text=True, timeout=300,
-                       env=env, cwd=ROOT)
+                        "--dist-backend", "gloo", "--no-cpu", "--frames", "200000", "--steps",
+                        "3", "--warmup", "1", "--min-warmup-s", "0", "--detail", detail],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads(r.stdout.strip().splitlines()[-1])
+    out = r.stdout.strip().splitlines()
+    assert len(out) == 1 and len(out[0]) < 8000, out
+    line = json.loads(out[0])
     assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "gloo"
+    assert set(line["extra"]) == {"config4", "config2_strong", "config3_strong"}
     assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
-    assert line["flow_reduce_via"] == "gloo"
+    assert line["flow_reduce_via"] == "gloo" and line["flow_reduce_verified"] is True
+    assert line["roofline"]["frac"] > 0 and line["cpu_baseline"] is None
+    with open(detail) as fh:
+        full = json.load(fh)
+    assert full["n_gpus"] == 2 and "roofline" in full["extra"]["config4"]
 
 
 RCCL_SCRIPT = r"""
@@ -199,6 +209,22 @@ torch.cuda.synchronize()
 assert np.array_equal(c.cpu().numpy(), host)
 rd.release_own_comms()
 dist.destroy_process_group()
+# the deadline join: world 1 joins at once (non-blocking communicator, polled) and its
+# all-reduce keeps the blocking contract; a world-2 id whose peer never comes is aborted
+# after the deadline and reports ncclInProgress (7), not a hang
+comm3 = engine.comm_init_timeout(1, engine.coll_unique_id(), 0, 20000)
+engine.flow_reduce(c, nb, comm3)
+torch.cuda.synchronize()
+assert np.array_equal(c.cpu().numpy(), host)
+engine.comm_destroy(comm3)
+import time
+t0 = time.time()
+try:
+    engine.comm_init_timeout(2, engine.coll_unique_id(), 0, 2000)
+    raise SystemExit("a world-2 init with no peer returned a communicator")
+except engine.RpktError as e:
+    assert engine.last_coll_error() == 7, (str(e), engine.last_coll_error())
+assert time.time() - t0 < 60, time.time() - t0
 print("own comm ok")
 """
 
