@@ -168,7 +168,8 @@ pub struct rpkt_fwd_t {
     pub smac: [u8; 6],
     pub forbid_dev: *const u32,
     pub n_forbid: u32,
-    pub reserved: u32,
+    /// 0, or RPKT_F_IPV6: also forward untagged IPv6/UDP frames
+    pub flags: u32,
 }
 
 /// One frame's option walks (TcpOptionsIter / Ipv4OptionsIter), 64 bytes.

@@ -408,13 +408,25 @@ int rpkt_gpu_build_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev, 
  * addresses, sorted ascending).  A forwarded frame is rewritten in place: ports and
  * addresses swapped, TTL - 1 (wrapping), dst/src MAC = dmac/smac, IPv4 and UDP
  * checksums recomputed (the reference's TX offload).  keep_dev[i] = 1 if forwarded;
- * other frames are not written.  frames_dev 16-byte aligned. */
+ * other frames are not written.  frames_dev 16-byte aligned.
+ * With fwd->flags = RPKT_F_IPV6 the parse also decodes IPv6 and an untagged IPv6/UDP
+ * frame is forwarded the same way: parsed OK with a valid L4 sum (a zero UDP checksum is
+ * invalid over IPv6), never matched against the (IPv4) forbidden list; addresses (16 B)
+ * and ports swapped, hop_limit - 1 (wrapping), MACs set, the UDP checksum updated over
+ * the IPv6 pseudo header (its destination stays a routing header's final address).
+ * IPv6 records are built by rpkt_gpu_build_batch as Ipv6::prepend_header + setters
+ * (ipv6/generated.rs:94-135): bytes 0..7 of the header from the record (ip6_vtcfl,
+ * payload_len = remaining, next_header, hop_limit), the addresses and the extension
+ * headers up to l4_off left as the buffer holds them (the record keeps the addresses
+ * folded), the L4 checksum over the IPv6 pseudo header (src, the address at
+ * ip6_pdst_off -- dst_addr when that offset does not lie in [l3 + 24, l4_off - 16] --,
+ * u32 length, next header), a UDP result of 0 sent as 0xffff. */
 typedef struct rpkt_fwd {
     uint8_t         dmac[6];
     uint8_t         smac[6];
     const uint32_t* forbid_dev;
     uint32_t        n_forbid;
-    uint32_t        reserved;
+    uint32_t        flags;      /* 0, or RPKT_F_IPV6 (was `reserved`, always 0) */
 } rpkt_fwd_t;
 int rpkt_gpu_forward_batch(const rpkt_batch_t* batch, const rpkt_fwd_t* fwd, uint8_t* keep_dev,
                            void* stream);

@@ -113,7 +113,8 @@ def lib():
         L.oracle_forward_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_uint32]
         L.oracle_forward_batch.restype = None
         L.oracle_options_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -238,8 +239,11 @@ def build_batch(frames, n, recs, flags=3, offsets=None, stride=0, frame_len=0):
     return out, built
 
 
-def forward_batch(frames, n, recs, dmac, smac, forbid=(), offsets=None, stride=0, frame_len=0):
-    """rpkt_gpu_forward_batch on the CPU: returns (new frames buffer, keep flags)."""
+def forward_batch(frames, n, recs, dmac, smac, forbid=(), offsets=None, stride=0, frame_len=0,
+                  flags=0):
+    """rpkt_gpu_forward_batch on the CPU: returns (new frames buffer, keep flags).  flags
+    (rpkt_fwd_t.flags): RPKT_F_IPV6 (8) also forwards IPv6 frames (recs from a parse with
+    RPKT_F_IPV6)."""
     out = np.array(frames, dtype=np.uint8, copy=True)
     recs = np.ascontiguousarray(recs)
     offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
@@ -249,7 +253,7 @@ def forward_batch(frames, n, recs, dmac, smac, forbid=(), offsets=None, stride=0
     keep = np.zeros(n, dtype=np.uint8)
     lib().oracle_forward_batch(_ptr(out), out.size, _ptr(offs), stride, frame_len, n, _ptr(recs),
                                _ptr(dm), _ptr(sm), _ptr(fb) if fb.size else None, fb.size,
-                               _ptr(keep))
+                               _ptr(keep), flags)
     return out, keep
 
 

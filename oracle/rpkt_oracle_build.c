@@ -20,9 +20,26 @@
  * over the header (IPv4) or pseudo header + segment (UDP/TCP); a UDP result of 0 is
  * sent as 0xffff (RFC 768).
  *
+ * IPv6 records (the record's IPv6 block, include/rpkt_gpu.h) are built the same way
+ * with Ipv6::prepend_header + setters (rpkt/src/ipv6/generated.rs:94-135) in place of
+ * the IPv4 ones: the 40-B template, payload_len = remaining() after the header
+ * (:96-105), set_version/traffic_class/flow_label from ip6_vtcfl (:107-123),
+ * set_next_header (:125), set_hop_limit (:129).  The record holds the addresses only
+ * folded, so the 32 address bytes are left as the buffer holds them (like option bytes),
+ * and so are the extension headers between the IPv6 header and l4_off (their own
+ * prepend_headers, :282, :425, :581, :743, are the caller's, as the IPv4 options are).
+ * The L4 checksum uses the IPv6 pseudo header (src, the address at ip6_pdst_off, u32
+ * upper-layer length, next header); a UDP result of 0 is sent as 0xffff, which over IPv6
+ * is mandatory (RFC 8200 section 8.1: a zero UDP checksum is never emitted).
+ *
  * Forward: rpkt-dpdk/examples/loopback_rx.rs:96-140 per frame, with the NIC's RX
  * checksum verdict bits (:99, :103, :108) replaced by the verify composition (the
  * record's ip_sum / l4_sum) and its TX checksum offload by a full recompute here.
+ * With ip6 set (rpkt_fwd_t.flags = RPKT_F_IPV6) an untagged IPv6/UDP frame is forwarded
+ * the same way: parsed OK, L4 sum valid (a zero UDP checksum is invalid over IPv6),
+ * source not forbidden (the list holds IPv4 addresses: an IPv6 source never matches);
+ * addresses and ports swapped, hop_limit - 1 (wrapping), MACs set, UDP checksum
+ * recomputed over the IPv6 pseudo header.
  */
 #include <stdint.h>
 #include <stddef.h>
@@ -35,6 +52,8 @@ int oracle_rec_is_ip6(const rpkt_rec_t* r);
 uint16_t oracle_combine(const uint16_t* checksums, size_t n);
 uint16_t oracle_pseudo_header_v4(const uint8_t* src4, const uint8_t* dst4, uint8_t proto,
                                  uint16_t length);
+uint16_t oracle_pseudo_header_v6(const uint8_t* src16, const uint8_t* dst16, uint8_t proto,
+                                 uint32_t length);
 
 static void put16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
 static void put32(uint8_t* p, uint32_t v) {
@@ -47,6 +66,97 @@ static const uint8_t TCP_T[20] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x50, 0, 0
 static const uint8_t IPV4_T[20] = {0x45, 0, 0, 0x14, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 static const uint8_t VLAN_T[4] = {0x00, 0x01, 0x08, 0x00};
 static const uint8_t ETHER_T[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x00};
+/* rpkt/src/ipv6/generated.rs:16-20 */
+static const uint8_t IPV6_T[40] = {0x60, 0, 0, 0, 0, 0, 0x04, 0};
+
+/* The IPv6 block of a record (include/rpkt_gpu.h: bytes 24..43 of an IPv6 record) */
+static uint32_t rec_u32(const rpkt_rec_t* r, int at) {
+    uint32_t v;
+    memcpy(&v, (const uint8_t*)r + at, 4);
+    return v;
+}
+static uint16_t rec_u16(const rpkt_rec_t* r, int at) {
+    uint16_t v;
+    memcpy(&v, (const uint8_t*)r + at, 2);
+    return v;
+}
+
+/* Udp|Tcp::prepend_header + setters at f + l4 (the L4 header bytes of the record) */
+static void emit_l4(uint8_t* f, uint32_t len, uint32_t l4, const rpkt_rec_t* r) {
+    if (r->ip_protocol == 17) {                             /* Udp::prepend_header :79-88 */
+        uint8_t* u = f + l4;
+        memcpy(u, UDP_T, 8);
+        put16(u + 4, len - l4);                             /* set_packet_len(remaining) */
+        put16(u + 0, r->src_port);                          /* set_src_port :90 */
+        put16(u + 2, r->dst_port);                          /* set_dst_port :94 */
+        put16(u + 6, r->l4_checksum);                       /* set_checksum */
+    } else if (r->ip_protocol == 6) {                       /* Tcp::prepend_header :135-141 */
+        uint8_t* t = f + l4;
+        memcpy(t, TCP_T, 20);
+        put16(t + 0, r->src_port);                          /* :148-155 */
+        put16(t + 2, r->dst_port);
+        put32(t + 4, r->tcp_seq);                           /* set_seq_num :156 */
+        put32(t + 8, r->tcp_ack);                           /* set_ack_num :160 */
+        put16(t + 12, r->l4_word6);                         /* header_len, reserved, flags :164-224 */
+        put16(t + 14, r->tcp_window);                       /* set_window_size :209 */
+        put16(t + 16, r->l4_checksum);                      /* set_checksum :213 */
+        put16(t + 18, r->tcp_urgent);                       /* set_urgent_pointer :217 */
+    }
+}
+
+/* [VlanFrame::prepend_header + setters]*, EtherFrame::prepend_header + setters */
+static void emit_link(uint8_t* f, uint32_t nv, const rpkt_rec_t* r) {
+    for (int k = (int)nv - 1; k >= 0; k--) {                /* VlanFrame::prepend_header :73-78 */
+        uint8_t* v = f + 14 + 4 * k;
+        memcpy(v, VLAN_T, 4);
+        put16(v, r->vlan_tci[k]);                           /* priority / dei / vlan_id */
+        put16(v + 2, r->vlan_ethertype[k]);                 /* set_ethertype */
+    }
+    memcpy(f, ETHER_T, 14);                                 /* EtherFrame::prepend_header :71-76 */
+    memcpy(f, r->dst_addr, 6);                              /* set_dst_addr :78 */
+    memcpy(f + 6, r->src_addr, 6);                          /* set_src_addr :82 */
+    put16(f + 12, r->ethertype);                            /* set_ethertype :86 */
+}
+
+/* The IPv6 record's build (Ipv6::prepend_header + setters, ipv6/generated.rs:94-135). */
+static int build_one6(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t flags) {
+    uint32_t nv = r->n_vlan;
+    uint32_t l3 = 14 + 4 * nv;
+    uint32_t l4 = r->l4_off;
+    uint32_t proto = r->ip_protocol;
+    uint32_t l4hdr = proto == 17 ? 8 : (proto == 6 ? (uint32_t)(r->l4_word6 >> 12) * 4 : 0);
+    if (l4 < l3 + 40) return 0;                             /* no IPv6 header parsed */
+    if (proto == 6 && l4hdr < 20) return 0;                 /* tcp/generated.rs:137 */
+    if (len < l4 + l4hdr) return 0;                         /* chunk_headroom asserts */
+    if (len - l3 - 40 > 65535) return 0;                    /* ipv6/generated.rs:99 */
+    if (proto == 17 && len - l4 > 65535) return 0;          /* udp/generated.rs:83 */
+    emit_l4(f, len, l4, r);
+    uint8_t* ip = f + l3;                                   /* Ipv6::prepend_header :96-105 */
+    uint8_t addrs[32];
+    memcpy(addrs, ip + 8, 32);                              /* the buffer's addresses */
+    memcpy(ip, IPV6_T, 40);
+    memcpy(ip + 8, addrs, 32);
+    put16(ip + 4, len - l3 - 40);                           /* set_payload_len(remaining) */
+    put32(ip, rec_u32(r, 24));                              /* version, traffic_class, flow_label */
+    ip[6] = ((const uint8_t*)r)[30];                        /* set_next_header :125 */
+    ip[7] = ((const uint8_t*)r)[31];                        /* set_hop_limit :129 */
+    emit_link(f, nv, r);
+    if ((flags & RPKT_BUILD_L4_CSUM) && (proto == 17 || proto == 6)) {
+        uint32_t pdst = rec_u16(r, 34);
+        /* an address the parse can report lies between dst_addr and the L4 header;
+         * any other value (a record no parse produced) falls back to dst_addr */
+        if (pdst < l3 + 24 || pdst + 16 > l4) pdst = l3 + 24;
+        uint32_t ck_off = proto == 17 ? 6 : 16;
+        uint32_t seg = len - l4;
+        put16(f + l4 + ck_off, 0);
+        uint16_t parts[2] = {oracle_pseudo_header_v6(ip + 8, f + pdst, (uint8_t)proto, seg),
+                             oracle_from_slice(f + l4, seg)};
+        uint16_t ck = (uint16_t)~oracle_combine(parts, 2);
+        if (proto == 17 && ck == 0) ck = 0xffff;            /* RFC 8200 section 8.1 */
+        put16(f + l4 + ck_off, ck);
+    }
+    return 1;
+}
 
 /* Build one frame of `len` bytes in place.  Returns 1 if written, 0 if the frame
  * cannot hold the headers the record asks for (where the reference's
@@ -54,7 +164,7 @@ static const uint8_t ETHER_T[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x
 int oracle_build_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t flags) {
     uint32_t nv = r->n_vlan;
     if (nv > RPKT_MAX_VLAN) return 0;
-    if (oracle_rec_is_ip6(r)) return 0;              /* the build writes IPv4 headers only */
+    if (oracle_rec_is_ip6(r)) return build_one6(f, len, r, flags);
     uint32_t l3 = 14 + 4 * nv;
     uint32_t ihl4 = (uint32_t)(r->ip_vhl & 0xf) * 4;
     uint32_t l4 = l3 + ihl4;
@@ -67,25 +177,7 @@ int oracle_build_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t fla
     if (proto == 17 && len - l4 > 65535) return 0;          /* udp/generated.rs:83 */
 
     /* cursor = l4 + l4hdr (the payload); build inside-out */
-    if (proto == 17) {                                      /* Udp::prepend_header :79-88 */
-        uint8_t* u = f + l4;
-        memcpy(u, UDP_T, 8);
-        put16(u + 4, len - l4);                             /* set_packet_len(remaining) */
-        put16(u + 0, r->src_port);                          /* set_src_port :90 */
-        put16(u + 2, r->dst_port);                          /* set_dst_port :94 */
-        put16(u + 6, r->l4_checksum);                       /* set_checksum */
-    } else if (proto == 6) {                                /* Tcp::prepend_header :135-141 */
-        uint8_t* t = f + l4;
-        memcpy(t, TCP_T, 20);
-        put16(t + 0, r->src_port);                          /* :148-155 */
-        put16(t + 2, r->dst_port);
-        put32(t + 4, r->tcp_seq);                           /* set_seq_num :156 */
-        put32(t + 8, r->tcp_ack);                           /* set_ack_num :160 */
-        put16(t + 12, r->l4_word6);                         /* header_len, reserved, flags :164-224 */
-        put16(t + 14, r->tcp_window);                       /* set_window_size :209 */
-        put16(t + 16, r->l4_checksum);                      /* set_checksum :213 */
-        put16(t + 18, r->tcp_urgent);                       /* set_urgent_pointer :217 */
-    }
+    emit_l4(f, len, l4, r);
     uint8_t* ip = f + l3;                                   /* Ipv4::prepend_header :130-140 */
     memcpy(ip, IPV4_T, 20);
     ip[0] = r->ip_vhl;                                      /* set_version / set_header_len */
@@ -98,16 +190,7 @@ int oracle_build_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t fla
     put16(ip + 10, r->ip_checksum);                         /* set_checksum */
     put32(ip + 12, r->ip_src);                              /* set_src_addr */
     put32(ip + 16, r->ip_dst);                              /* set_dst_addr */
-    for (int k = (int)nv - 1; k >= 0; k--) {                /* VlanFrame::prepend_header :73-78 */
-        uint8_t* v = f + 14 + 4 * k;
-        memcpy(v, VLAN_T, 4);
-        put16(v, r->vlan_tci[k]);                           /* priority / dei / vlan_id */
-        put16(v + 2, r->vlan_ethertype[k]);                 /* set_ethertype */
-    }
-    memcpy(f, ETHER_T, 14);                                 /* EtherFrame::prepend_header :71-76 */
-    memcpy(f, r->dst_addr, 6);                              /* set_dst_addr :78 */
-    memcpy(f + 6, r->src_addr, 6);                          /* set_src_addr :82 */
-    put16(f + 12, r->ethertype);                            /* set_ethertype :86 */
+    emit_link(f, nv, r);
 
     if (flags & RPKT_BUILD_IP_CSUM) {                       /* TX IP checksum offload */
         put16(ip + 10, 0);
@@ -151,11 +234,43 @@ void oracle_build_batch(uint8_t* frames, uint64_t frames_bytes, const uint32_t* 
     }
 }
 
+/* The IPv6 counterpart of the loopback_rx rewrite (rpkt_fwd_t.flags & RPKT_F_IPV6):
+ * an untagged IPv6/UDP frame that parsed OK with a valid L4 sum. */
+static int forward_one6(uint8_t* f, uint32_t len, const rpkt_rec_t* r, const uint8_t* dmac,
+                        const uint8_t* smac) {
+    if (r->n_vlan) return 0;                               /* :101 ethertype() == IPV6 */
+    if (r->ip_protocol != 17) return 0;                    /* :106 next header UDP */
+    if (r->l4_sum != 0xffff) return 0;                     /* :107 L4 good (no 0 exemption) */
+    uint32_t l3 = r->l3_off, l4 = r->l4_off;
+    if (len < l4 + 8) return 0;
+    uint8_t* ip = f + l3;
+    uint8_t* u = f + l4;
+    uint8_t a[16];
+    put16(u + 0, r->dst_port);                             /* swap ports */
+    put16(u + 2, r->src_port);
+    memcpy(a, ip + 8, 16);                                 /* swap addresses */
+    memcpy(ip + 8, ip + 24, 16);
+    memcpy(ip + 24, a, 16);
+    ip[7] = (uint8_t)(ip[7] - 1);                          /* hop_limit - 1 (wrapping) */
+    memcpy(f, dmac, 6);
+    memcpy(f + 6, smac, 6);
+    uint32_t pdst = rec_u16(r, 34);                        /* final address (routing header) */
+    uint32_t seg = (uint32_t)r->l4_word6;                  /* the UDP datagram (length field) */
+    put16(u + 6, 0);
+    uint16_t parts[2] = {oracle_pseudo_header_v6(ip + 8, f + pdst, 17, seg),
+                         oracle_from_slice(u, seg)};
+    uint16_t ck = (uint16_t)~oracle_combine(parts, 2);
+    put16(u + 6, ck == 0 ? 0xffff : ck);
+    return 1;
+}
+
 /* loopback_rx.rs:96-140 over one parsed frame.  Returns 1 when the frame is
- * forwarded (rewritten in place), 0 when the reference would drop it. */
+ * forwarded (rewritten in place), 0 when the reference would drop it.  ip6: also
+ * forward IPv6 frames (records of an RPKT_F_IPV6 parse). */
 int oracle_forward_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, const uint8_t* dmac,
-                       const uint8_t* smac, const uint32_t* forbid, uint32_t n_forbid) {
+                       const uint8_t* smac, const uint32_t* forbid, uint32_t n_forbid, int ip6) {
     if (r->status != RPKT_S_OK) return 0;                  /* every parse Ok */
+    if (ip6 && oracle_rec_is_ip6(r)) return forward_one6(f, len, r, dmac, smac);
     if (r->ethertype != 0x0800 || r->n_vlan) return 0;     /* :101 ethertype() == IPV4 */
     if (r->ip_sum != 0xffff) return 0;                     /* :101 rx_offload IP good */
     if (r->ip_protocol != 17) return 0;                    /* :106 protocol() == UDP */
@@ -188,11 +303,12 @@ int oracle_forward_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, const uint
 void oracle_forward_batch(uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
                           uint32_t stride, uint32_t frame_len, uint32_t n, const rpkt_rec_t* recs,
                           const uint8_t* dmac, const uint8_t* smac, const uint32_t* forbid,
-                          uint32_t n_forbid, uint8_t* keep) {
+                          uint32_t n_forbid, uint8_t* keep, uint32_t fwd_flags) {
     for (uint32_t i = 0; i < n; i++) {
         uint64_t off, len;
         span(frames_bytes, offsets, stride, frame_len, i, &off, &len);
         keep[i] = (uint8_t)oracle_forward_one(frames + off, (uint32_t)len, &recs[i], dmac, smac,
-                                              forbid, n_forbid);
+                                              forbid, n_forbid,
+                                              (fwd_flags & RPKT_F_IPV6) != 0);
     }
 }

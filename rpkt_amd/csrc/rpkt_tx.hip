@@ -63,14 +63,12 @@ __device__ __forceinline__ void put_be32(uint8_t* p, uint32_t v) {
 }
 
 // Fixed header bytes from record words (include/rpkt_gpu.h layout): Ethernet, n_vlan
-// tags, the 20 IPv4 bytes at l3, the UDP header or the 20 TCP bytes at l4.  These
-// are exactly the bytes prepend_header + setters write (ether/generated.rs:71-88,
-// vlan/generated.rs:73-100, ipv4/generated.rs:130-206, udp/generated.rs:79-104,
-// tcp/generated.rs:135-224); option bytes are not touched.
-__device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20], uint32_t nv,
-                                             uint32_t l3, uint32_t l4, uint32_t proto,
-                                             uint32_t ip_len, uint32_t udp_len, uint32_t ip_ck,
-                                             uint32_t l4_ck) {
+// tags, the 20 IPv4 bytes at l3 (or the IPv6 header's first 8 bytes), the UDP header or
+// the 20 TCP bytes at l4.  These are exactly the bytes prepend_header + setters write
+// (ether/generated.rs:71-88, vlan/generated.rs:73-100, ipv4/generated.rs:130-206,
+// ipv6/generated.rs:94-135, udp/generated.rs:79-104, tcp/generated.rs:135-224); option
+// bytes, IPv6 addresses and extension headers are not touched.
+__device__ __forceinline__ void emit_link(uint8_t* s, const uint32_t (&w)[20], uint32_t nv) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) s[k] = (uint8_t)(w[1 + k / 4] >> (8 * (k % 4)));
     put_be16(s + 12, w[0] >> 16);
@@ -81,7 +79,9 @@ __device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20]
             put_be16(s + 16 + 4 * v, w[5] >> (16 * v));
         }
     }
-    uint8_t* ip = s + l3;
+}
+__device__ __forceinline__ void emit_ip4(uint8_t* ip, const uint32_t (&w)[20], uint32_t ip_len,
+                                         uint32_t ip_ck) {
     ip[0] = (uint8_t)w[6];
     ip[1] = (uint8_t)(w[6] >> 8);
     put_be16(ip + 2, ip_len);
@@ -92,7 +92,18 @@ __device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20]
     put_be16(ip + 10, ip_ck);
     put_be32(ip + 12, w[9]);
     put_be32(ip + 16, w[10]);
-    uint8_t* t = s + l4;
+}
+// Ipv6::prepend_header + setters: version / traffic class / flow label (ip6_vtcfl),
+// payload_len = remaining() after the header, next_header, hop_limit
+__device__ __forceinline__ void emit_ip6(uint8_t* ip, const uint32_t (&w)[20], uint32_t plen) {
+    put_be32(ip, w[6]);
+    put_be16(ip + 4, plen);
+    ip[6] = (uint8_t)(w[7] >> 16);
+    ip[7] = (uint8_t)(w[7] >> 24);
+}
+// `t` is the LDS slot, or global memory for an IPv6 L4 header past the window
+__device__ __forceinline__ void emit_l4(uint8_t* t, const uint32_t (&w)[20], uint32_t proto,
+                                        uint32_t udp_len, uint32_t l4_ck) {
     if (proto == 17u) {
         put_be16(t, w[11]);
         put_be16(t + 2, w[11] >> 16);
@@ -108,6 +119,14 @@ __device__ __forceinline__ void emit_headers(uint8_t* s, const uint32_t (&w)[20]
         put_be16(t + 16, l4_ck);
         put_be16(t + 18, w[15] >> 16);
     }
+}
+// The word sum of the L4 header emit_l4 writes, with its checksum field 0 (big-endian
+// words from the record's host-order values)
+__device__ __forceinline__ uint32_t l4_hdr_sum(const uint32_t (&w)[20], uint32_t proto,
+                                               uint32_t udp_len) {
+    const uint32_t ports = halves(w[11]);
+    return proto == 17u ? ports + udp_len
+                        : ports + halves(w[12]) + halves(w[13]) + halves(w[14]) + (w[15] >> 16);
 }
 
 // Absolute-phase word sum of LDS slot bytes [s, e) (any alignment): whole dwords,
@@ -232,6 +251,15 @@ __device__ __forceinline__ uint32_t line_end(Frame fr, uint32_t hdr_end) {
     return e < kWin - ph ? e : kWin - ph;
 }
 
+// End (frame-relative) of the 16-B chunk holding header byte hdr_end - 1: the least
+// whole-chunk range covering the rewritten bytes, clipped to the frame and the window.
+__device__ __forceinline__ uint32_t chunk_end(Frame fr, uint32_t hdr_end) {
+    const uint32_t ph = fr.off & 15u;
+    const uint32_t c = ((fr.off + hdr_end + 15u) & ~15u) - fr.off;
+    uint32_t e = c < fr.len ? c : fr.len;
+    return e < kWin - ph ? e : kWin - ph;
+}
+
 // rpkt_gpu_build_batch: window -> headers composed in LDS -> checksums (IPv4 over the
 // slot; L4 over the slot plus the payload stream past the window) -> write-back.
 template <bool L4FILL>
@@ -267,26 +295,34 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     uint8_t* slot = &W.win[lane * kSlot];
     const uint32_t nv = (w[0] >> 8) & 0xffu;
     const uint32_t l3 = 14u + 4u * nv;
-    const uint32_t ihl4 = (w[6] & 0xfu) * 4u;
-    const uint32_t l4 = l3 + ihl4;
-    const uint32_t proto = (w[8] >> 8) & 0xffu;
-    const uint32_t doff4 = ((w[14] >> 12) & 0xfu) * 4u;
-    const uint32_t l4hdr = proto == 17u ? 8u : (proto == 6u ? doff4 : 0u);
-    const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
-    // the build writes IPv4 headers: an IPv6 record (RPKT_F_IPV6 parse: dispatched on
-    // 0x86DD) is not built
+    // an IPv6 record (RPKT_F_IPV6 parse: dispatched on 0x86DD) is built with the IPv6
+    // header; its l4 is the record's (after the extension headers)
     const uint32_t st = w[0] & 0xffu;
     const uint32_t det = nv == 0u ? w[0] >> 16 : (nv == 1u ? w[5] & 0xffffu : w[5] >> 16);
     const bool rec6 = det == 0x86ddu && st != RPKT_S_ETH_SHORT && st != RPKT_S_VLAN_SHORT &&
                       st != RPKT_S_NOT_IPV4;
-    const bool ok = valid && !rec6 && nv <= RPKT_MAX_VLAN && ihl4 >= 20u && !(proto == 6u && doff4 < 20u) &&
-                    len >= l4 + l4hdr && len - l3 <= 65535u &&
-                    !(proto == 17u && len - l4 > 65535u);
-    const bool fill_ip = ok && (flags & RPKT_BUILD_IP_CSUM);
+    const uint32_t ihl4 = (w[6] & 0xfu) * 4u;
+    const uint32_t l4 = rec6 ? w[16] >> 16 : l3 + ihl4;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;                 // byte 33 in both layouts
+    const uint32_t doff4 = ((w[14] >> 12) & 0xfu) * 4u;
+    const uint32_t l4hdr = proto == 17u ? 8u : (proto == 6u ? doff4 : 0u);
+    const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
+    const bool fits = valid && nv <= RPKT_MAX_VLAN && !(proto == 6u && doff4 < 20u) &&
+                      len >= l4 + l4hdr && !(proto == 17u && len - l4 > 65535u);
+    const bool ok = fits && (rec6 ? l4 >= l3 + 40u && len - l3 - 40u <= 65535u
+                                  : ihl4 >= 20u && len - l3 <= 65535u);
+    // an IPv6 L4 header that does not lie whole in the window is written to global memory
+    // by its lane (extension headers can push it past the window), never from the slot
+    const bool far = ok && rec6 && fixed4 != 0u && ph + l4 + fixed4 > (uint32_t)kWin;
+    const bool fill_ip = ok && !rec6 && (flags & RPKT_BUILD_IP_CSUM);
     const bool fill_l4 = L4FILL && ok && fixed4;
-    if (ok)
-        emit_headers(slot + ph, w, nv, l3, l4, proto, len - l3, len - l4,
-                     fill_ip ? 0u : (w[8] >> 16), fill_l4 ? 0u : (w[15] & 0xffffu));
+    if (ok) {
+        emit_link(slot + ph, w, nv);
+        if (rec6) emit_ip6(slot + ph + l3, w, len - l3 - 40u);
+        else emit_ip4(slot + ph + l3, w, len - l3, fill_ip ? 0u : (w[8] >> 16));
+        emit_l4(far ? frames + fr.off + l4 : slot + ph + l4, w, proto, len - l4,
+                fill_l4 ? 0u : (w[15] & 0xffffu));
+    }
     if (fill_ip) {
         const uint32_t s = be_sum(lds_range_sum(slot, ph + l3, ph + l4), fr.off + l3);
         put_be16(slot + ph + l3 + 10, ~s & 0xffffu);
@@ -295,38 +331,53 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         // everything the checksum needs after the stream is packed into the slot's
         // spare dword (bytes 128..131) and two registers, so the stream keeps its
         // registers: pseudo header sum, in-window part, and
-        // info = fill | udp << 1 | l4 slot offset << 8
+        // info = fill | udp << 1 | far << 2 | l4 slot offset << 8
         uint32_t part = 0, ss = 0, se = 0, pseudo = 0;
         const uint32_t win_end = kWin - ph;
         if (fill_l4) {
+            // the summed range starts at the L4 header, or past it (far: the header's
+            // sum comes from the record's values); the in-window part, then the stream
+            const uint32_t ps = far ? l4 + fixed4 : l4;
             const uint32_t e_in = len < win_end ? len : win_end;
-            part = lds_range_sum(slot, ph + l4, ph + e_in);
-            if (len > e_in) {
-                ss = fr.off + e_in;
+            part = ps < e_in ? lds_range_sum(slot, ph + ps, ph + e_in) : 0u;
+            const uint32_t s0 = ps > e_in ? ps : e_in;
+            if (len > s0) {
+                ss = fr.off + s0;
                 se = fr.off + len;
             }
-            const uint32_t src = w[9], dst = w[10];
-            pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + proto +
-                     (len - l4);
+            if (rec6) {                 // pseudo_v6: src, the final destination, length, nh
+                const FrameDw dw{slot, ph, fr.off, fb, rs};
+                uint32_t pd = w[8] >> 16;
+                if (pd < l3 + 24u || pd + 16u > l4) pd = l3 + 24u;   // as the oracle
+                pseudo = addr_words_sum(dw(l3 + 8u), dw(l3 + 12u), dw(l3 + 16u), dw(l3 + 20u)) +
+                         addr_words_sum(dw(pd), dw(pd + 4u), dw(pd + 8u), dw(pd + 12u));
+            } else {
+                const uint32_t src = w[9], dst = w[10];
+                pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu);
+            }
+            pseudo += proto + (len - l4) + (far ? l4_hdr_sum(w, proto, len - l4) : 0u);
         }
-        *reinterpret_cast<uint32_t*>(slot + kWin) =
-            (uint32_t)fill_l4 | ((uint32_t)(proto == 17u) << 1) | ((ph + l4) << 8);
+        *reinterpret_cast<uint32_t*>(slot + kWin) = (uint32_t)fill_l4 |
+            ((uint32_t)(proto == 17u) << 1) | ((uint32_t)far << 2) | ((ph + l4) << 8);
         uint32_t sp = 0;
         if constexpr (!kWholeFrame) sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
         const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
         if (info & 1u) {
             const uint32_t at = info >> 8;                      // slot offset of the L4 header
+            // (far: the summed range starts fixed4 bytes later, an even offset: same phase)
             const uint32_t sum = fold16(pseudo + be_sum(part + sp, (fr.off & ~15u) + at));
             uint32_t ck = ~sum & 0xffffu;
             const bool udp = info & 2u;
-            if (udp && ck == 0u) ck = 0xffffu;                  // RFC 768
-            put_be16(slot + at + (udp ? 6u : 16u), ck);
+            if (ck == 0u && udp) ck = 0xffffu;                  // RFC 768 / RFC 8200 8.1
+            uint8_t* t = (info & 4u) ? frames + (fr.off & ~15u) + at : slot + at;
+            put_be16(t + (udp ? 6u : 16u), ck);
         }
     }
     wave_sync();
     // the window holds the original bytes around the headers: round the written range
     // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
-    const uint32_t r1 = ok ? line_end(fr, l4 + fixed4) : 0u;
+    uint32_t r1 = ok ? line_end(fr, far ? l3 + 8u : l4 + fixed4) : 0u;
+    r1 = far && r1 > l4 ? l4 : r1;                          // the L4 header went to memory
     write_back(rs, frames, W, lane, fr.off, r1);
     if (built && valid) built[i] = ok ? 1 : 0;
 }
@@ -344,6 +395,9 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
 // 4 = default-policy window loads).
 #ifndef RPKT_FWD_WB_AUX
 #define RPKT_FWD_WB_AUX 3        // forward's write-back stores: sc0 | nt
+#endif
+#ifndef RPKT_FWD_WB_CHUNKS
+#define RPKT_FWD_WB_CHUNKS 0     // 1: write back only the 16-B chunks holding rewritten bytes
 #endif
 #ifndef RPKT_FWD_WAVES_W64
 #define RPKT_FWD_WAVES_W64 5     // 64-B windows: LDS allows 6 waves per SIMD; 5 -> <= 96 VGPRs
@@ -391,47 +445,87 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
         return;
     }
     LaneRec L;
-    parse_lane(W, lane, fr, valid, V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM), L, rs,
-               fb);
+    parse_lane(W, lane, fr, valid,
+               (V == 2 ? RPKT_F_IP_SUM : (RPKT_F_IP_SUM | RPKT_F_L4_SUM)) | (fwd.flags & RPKT_F_IPV6),
+               L, rs, fb);
     uint8_t* slot = &W.win[lane * kSlot];
     uint8_t* s = slot + (fr.off & 15u);
+    const uint32_t l4 = L.w[16] >> 16;
+    uint32_t delta = 0;                 // IPv6 pseudo header change (one's-complement add)
+    bool far = false;                   // IPv6: UDP header not whole in the window
     {
         // loopback_rx.rs:99-106 before the L4 sum is known: Ok chain, untagged IPv4
         // (w0 = status | n_vlan << 8 | ethertype << 16), IP checksum good, UDP.  The
         // rewrite that does not depend on the L4 sum is done in the window now
         // (written back only if the frame is kept); what the rest needs waits in the
-        // slot's spare dword: pre | l4 << 8 | udp checksum << 16.
+        // slot's spare dword: pre | far << 1 | udp checksum << 16.
         const uint32_t w0 = L.w[0], w8 = L.w[8], w9 = L.w[9], w10 = L.w[10], w11 = L.w[11];
-        const uint32_t ip_sum = L.w[18] & 0xffffu, l4 = L.w[16] >> 16;
-        const bool pre = valid && (w0 & 0xffffu) == RPKT_S_OK && (w0 >> 16) == 0x0800u &&
-                         ip_sum == 0xffffu && ((w8 >> 8) & 0xffu) == 17u;
-        if (pre) {                                              // loopback_rx.rs:120-133
-            const uint32_t ttl = w8 & 0xffu;
-            const uint32_t old_w = (ttl << 8) | 17u, new_w = (((ttl - 1u) & 0xffu) << 8) | 17u;
-            const uint32_t ip_ck = ~fold16(ip_sum + (~(w8 >> 16) & 0xffffu) +
-                                           (~old_w & 0xffffu) + new_w) & 0xffffu;
+        const uint32_t ip_sum = L.w[18] & 0xffffu;
+        const bool pre4 = valid && !L.is6 && (w0 & 0xffffu) == RPKT_S_OK && (w0 >> 16) == 0x0800u &&
+                          ip_sum == 0xffffu && ((w8 >> 8) & 0xffu) == 17u;
+        // the IPv6 counterpart (fwd.flags & RPKT_F_IPV6): untagged (the record's n_vlan 0,
+        // ethertype 0x86DD), parsed OK to UDP; there is no header checksum
+        const bool pre6 = valid && L.is6 && (w0 & 0xffffu) == RPKT_S_OK && ((w8 >> 8) & 0xffu) == 17u;
+        if (pre4 || pre6) {                                     // loopback_rx.rs:120-133
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
                 s[k] = fwd.dmac[k];
                 s[6 + k] = fwd.smac[k];
             }
+        }
+        if (pre4) {
+            const uint32_t ttl = w8 & 0xffu;
+            const uint32_t old_w = (ttl << 8) | 17u, new_w = (((ttl - 1u) & 0xffu) << 8) | 17u;
+            const uint32_t ip_ck = ~fold16(ip_sum + (~(w8 >> 16) & 0xffffu) +
+                                           (~old_w & 0xffffu) + new_w) & 0xffffu;
             s[22] = (uint8_t)(ttl - 1u);
             put_be16(s + 24, ip_ck);
             put_be32(s + 26, w10);
             put_be32(s + 30, w9);
             put_be16(s + l4, w11 >> 16);
             put_be16(s + l4 + 2, w11);
+        } else if (pre6) {
+            // hop_limit - 1, the addresses swapped (bytes 8..39 of the header, 54 at most:
+            // in the window), the ports swapped in the window or, past it, after the stream
+            constexpr uint32_t l3 = 14u;
+            s[l3 + 7] = (uint8_t)(s[l3 + 7] - 1u);
+            uint32_t a[4], b[4];
+            const FrameDw dw{slot, fr.off & 15u, fr.off, fb, rs};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a[k] = dw(l3 + 8u + 4u * k);
+                b[k] = dw(l3 + 24u + 4u * k);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                s[l3 + 8 + k] = (uint8_t)(b[k / 4] >> (8 * (k % 4)));
+                s[l3 + 24 + k] = (uint8_t)(a[k / 4] >> (8 * (k % 4)));
+            }
+            // the pseudo header's destination is the final address of a routing header
+            // when there is one (record ip6_pdst_off != dst_addr): the swap then moves the
+            // old dst into the source slot only, a change of S(dst) - S(src)
+            if ((w8 >> 16) != l3 + 24u) {
+                const uint32_t sa = fold16(addr_words_sum(a[0], a[1], a[2], a[3]));
+                const uint32_t sb = fold16(addr_words_sum(b[0], b[1], b[2], b[3]));
+                delta = sb + (~sa & 0xffffu);
+            }
+            far = (fr.off & 15u) + l4 + 8u > (uint32_t)kWin;
+            if (!far) {
+                put_be16(s + l4, w11 >> 16);
+                put_be16(s + l4 + 2, w11);
+            }
         }
         *reinterpret_cast<uint32_t*>(slot + kWin) =
-            (uint32_t)pre | (l4 << 8) | ((L.w[15] & 0xffffu) << 16);
+            (uint32_t)(pre4 || pre6) | ((uint32_t)far << 1) | ((L.w[15] & 0xffffu) << 16);
     }
     uint32_t sp = 0;
     if constexpr (!kWholeFrame) sp = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
     const uint32_t l4_sum =
         L.want_l4 ? fold16(L.pseudo + be_sum(L.l4_part + sp, L.l4_start_abs)) : 0u;
     const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
-    const uint32_t l4 = (info >> 8) & 0xffu, udp_ck = info >> 16;
-    bool fwd_ok = (info & 1u) && (l4_sum == 0xffffu || udp_ck == 0u);   // :107 L4 good
+    const uint32_t udp_ck = info >> 16;
+    // :107 L4 good (over IPv6 a zero UDP checksum is not "not computed", RFC 8200 8.1)
+    bool fwd_ok = (info & 1u) && (l4_sum == 0xffffu || (udp_ck == 0u && !L.is6));
     if (fwd.n_forbid) {                                         // :111-118, sorted list
         // up to 128 addresses are searched in LDS (W.s and W.e, contiguous, free once
         // the stream is done), a longer list in global memory
@@ -443,7 +537,8 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
             wave_sync();
             list = t;
         }
-        if (fwd_ok) {
+        // the list holds IPv4 addresses: an IPv6 source never matches it
+        if (fwd_ok && !L.is6) {
             const uint32_t src = ((uint32_t)s[30] << 24) | ((uint32_t)s[31] << 16) |
                                  ((uint32_t)s[32] << 8) | s[33];   // swapped: old source
             uint32_t lo = 0, hi = fwd.n_forbid;
@@ -457,10 +552,21 @@ void forward_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* _
     }
     uint32_t r1 = 0;
     if (fwd_ok) {
-        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu)) & 0xffffu;
+        uint32_t u_ck = ~fold16(l4_sum + (~udp_ck & 0xffffu) + delta) & 0xffffu;
         if (u_ck == 0u) u_ck = 0xffffu;                         // RFC 768
-        put_be16(s + l4 + 6, u_ck);
-        r1 = line_end(fr, l4 + 8u);
+        if (info & 2u) {
+            // IPv6 UDP header past the window: ports and checksum stored by the lane (the
+            // stream that read those bytes is done), the write-back stops before them
+            uint8_t* g = frames + fr.off + l4;
+            put_be16(g, L.w[11] >> 16);
+            put_be16(g + 2, L.w[11]);
+            put_be16(g + 6, u_ck);
+            r1 = line_end(fr, 54u);
+            r1 = r1 > l4 ? l4 : r1;
+        } else {
+            put_be16(s + l4 + 6, u_ck);
+            r1 = RPKT_FWD_WB_CHUNKS ? chunk_end(fr, l4 + 8u) : line_end(fr, l4 + 8u);
+        }
     }
     wave_sync();
     // the rewritten lines are not read again: streaming stores (forward 2: 27.8 -> 26.2 us

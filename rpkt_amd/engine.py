@@ -46,7 +46,7 @@ class Fwd(ctypes.Structure):
     """rpkt_fwd_t"""
     _fields_ = [("dmac", ctypes.c_uint8 * 6), ("smac", ctypes.c_uint8 * 6),
                 ("forbid_dev", ctypes.c_void_p), ("n_forbid", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32)]
 
 
 EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name",
@@ -494,15 +494,17 @@ def forbid_list(addrs, device="cuda"):
     return torch.from_numpy(a.view(np.int32).copy()).to(device)
 
 
-def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None):
+def forward_batch(batch, dmac, smac, forbid=None, keep=None, stream=None, flags=0):
     """rpkt_gpu_forward_batch (loopback_rx firewall: parse, verdict, rewrite in place).
-    forbid: None or a tensor from forbid_list()."""
+    forbid: None or a tensor from forbid_list(); flags: 0 or RPKT_F_IPV6 (8), which also
+    forwards untagged IPv6/UDP frames."""
     torch = _torch()
     if keep is None:
         keep = torch.empty(batch.n, dtype=torch.uint8, device=batch.frames.device)
     f = Fwd()
     f.dmac[:] = list(bytes(dmac))
     f.smac[:] = list(bytes(smac))
+    f.flags = flags
     if forbid is not None and forbid.numel():
         if forbid.dtype != torch.int32:
             raise RpktError("forbid must come from forbid_list() (sorted u32 as int32)")

@@ -8,7 +8,9 @@ stream).  Events order the stages, so with S slots the upload of group k + 1 and
 download of group k - 1 overlap the parse of group k, and up to S - 1 uploads can be
 queued ahead of the parse.  A group is `group` consecutive batches of the ring, moved
 by ONE hipMemcpyAsync each way: at 64-B frames a 1M-frame batch is only 64 MiB, and the
-fixed cost of a copy is then a visible share of its time.
+fixed cost of a copy is then a visible share of its time.  The group's batches are parsed
+by ONE rpkt_gpu_parse_ring[_compact] launch (use_ring=True, the default), so the per-launch
+fixed cost (launch gap and drain) is paid once per copy group too.
 
 The rate is PCIe-bound (Gen5 x16: 63 GB/s per direction on paper), far below the
 device-resident rate: bench.py reports it under extra.host_inclusive, never as the
@@ -22,9 +24,11 @@ from . import engine, gen
 from .records import REC16_BYTES, REC_BYTES
 
 
-def host_inclusive(cfg, compact=False, steps=12, slots=3, group=1, n=None, seed=None):
+def host_inclusive(cfg, compact=False, steps=12, slots=3, group=1, n=None, seed=None,
+                   use_ring=True):
     """Time `steps` pipeline steps of config `cfg` (strided configs 2 / 3, or a packed
-    config) with `group` batches of n frames per copy and `slots` device buffers.
+    config) with `group` batches of n frames per copy and `slots` device buffers; the
+    group's batches parsed by one ring launch (use_ring) or one launch each.
     Returns the rates (whole-pipeline frames/s and the bytes each direction moved)."""
     import torch
     hb = gen.make_batch(cfg, n, seed=seed)
@@ -44,13 +48,28 @@ def host_inclusive(cfg, compact=False, steps=12, slots=3, group=1, n=None, seed=
         else [None] * slots
     dev_recs = [torch.empty(group * hb.n * rb, dtype=torch.uint8, device="cuda") for _ in range(slots)]
     parse = engine.parse_batch_compact if compact else engine.parse_batch
+    # the device batches of every slot's group, and (use_ring) their rpkt_ring_slot_t arrays
+    dbs = []
+    for b in range(slots):
+        row = []
+        for g in range(group):
+            if offs is not None:
+                row.append(engine.DeviceBatch(dev_frames[b], hb.n, dev_offs[b][g * (hb.n + 1):
+                                                                            (g + 1) * (hb.n + 1)]))
+            else:
+                row.append(engine.DeviceBatch(dev_frames[b][g * fb:(g + 1) * fb], hb.n, None,
+                                              hb.stride, hb.frame_len))
+        dbs.append(row)
+    recs_of = [[dev_recs[b][g * hb.n * rb:(g + 1) * hb.n * rb] for g in range(group)]
+               for b in range(slots)]
+    rings = [engine.ring_slots(dbs[b], recs_of[b], compact=compact) for b in range(slots)] \
+        if use_ring else None
     s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     up = [torch.cuda.Event() for _ in range(slots)]
     done = [torch.cuda.Event() for _ in range(slots)]
     down = [torch.cuda.Event() for _ in range(slots)]
     for e in done + down:
         e.record(s_out)
-    no = hb.n + 1
 
     def step(k):
         b = k % slots
@@ -62,13 +81,11 @@ def host_inclusive(cfg, compact=False, steps=12, slots=3, group=1, n=None, seed=
             up[b].record(s_in)
         s_cmp.wait_event(up[b])
         s_cmp.wait_event(down[b])               # the slot's previous records are home
-        for g in range(group):
-            if offs is not None:
-                db = engine.DeviceBatch(dev_frames[b], hb.n, dev_offs[b][g * no:(g + 1) * no])
-            else:
-                db = engine.DeviceBatch(dev_frames[b][g * fb:(g + 1) * fb], hb.n, None,
-                                        hb.stride, hb.frame_len)
-            parse(db, flags, recs=dev_recs[b][g * hb.n * rb:(g + 1) * hb.n * rb], stream=s_cmp)
+        if use_ring:
+            engine.parse_ring(rings[b], flags, stream=s_cmp, compact=compact)
+        else:
+            for g in range(group):
+                parse(dbs[b][g], flags, recs=recs_of[b][g], stream=s_cmp)
         done[b].record(s_cmp)
         with torch.cuda.stream(s_out):
             s_out.wait_event(done[b])
@@ -88,6 +105,7 @@ def host_inclusive(cfg, compact=False, steps=12, slots=3, group=1, n=None, seed=
     h2d = (int(ring.numel()) + (int(offs.numel()) * 4 if offs is not None else 0)) * steps
     d2h = int(host_recs.numel()) * steps
     return {"config": cfg, "record_bytes": rb, "slots": slots, "batches_per_copy": group,
+            "parse": "ring" if use_ring else "per batch",
             "frames_per_batch": hb.n, "steps": steps, "mpps": frames / dt / 1e6,
             "frame_gb_per_s": fbytes / dt / 1e9, "h2d_gb_per_s": h2d / dt / 1e9,
             "d2h_gb_per_s": d2h / dt / 1e9, "ms_per_copy": dt / steps * 1e3,

@@ -134,3 +134,15 @@ def test_compact_ring_of_short_strided_frames(torch):
             want = project16(o, flags).tobytes()
             assert recs[k][:hb.n * 16].cpu().numpy().tobytes() == want, (flags, k)
             assert np.array_equal(evs[k][:hb.n].cpu().numpy().view(np.uint64), ev), (flags, k)
+
+
+@pytest.mark.parametrize("cfg,compact", [(2, False), (2, True), (4, False), (10, True)])
+def test_host_pipeline_ring_and_per_batch(torch, cfg, compact):
+    """rpkt_amd.pipeline: pinned H2D of a copy group -> one parse_ring launch over the
+    group's batches (or one parse per batch) -> D2H of the records; the records that come
+    home equal the per-batch device parse (records_checked) either way."""
+    from rpkt_amd import pipeline
+    for use_ring in (True, False):
+        r = pipeline.host_inclusive(cfg, compact, steps=3, slots=2, group=3, n=20000,
+                                    use_ring=use_ring)
+        assert r["records_checked"] is True and r["parse"] == ("ring" if use_ring else "per batch")
