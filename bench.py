@@ -45,8 +45,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from rpkt_amd import dist as rdist, engine, fields, gen  # noqa: E402
-from rpkt_amd.records import (LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, as_records,  # noqa: E402
-                              is_ip6)
+from rpkt_amd.records import (LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, F_IPV6,  # noqa: E402
+                              as_records, is_ip6)
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -566,7 +566,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
     # the records of batch 0 are read back before the copy references overwrite them
     g = as_records(recs[0].cpu().numpy()) if cpu and rank == 0 and not compact and not opts \
         else None
-    if cfg == 2 and main and not compact and not strong:
+    if cfg == 2 and main and not compact and not strong and world == 1:
         try:
             out["copy_ceiling"] = copy_ceiling(dbs, recs, args.steps)
         except engine.RpktError as e:           # the development library is optional
@@ -838,8 +838,10 @@ def run_tx(cfg, mode, args, rank, world):
     resident batch whose records come from rpkt_gpu_parse_batch.  Rotates over 8
     batches at 64 B like config 2.  Algorithmic bytes per frame: build = 80 B record
     read + the frame read once (checksums) + the fixed header bytes written;
-    forward (fused parse + verdict + rewrite) = the frame read once + the 42 rewritten
-    header bytes of forwarded frames + 1 B verdict."""
+    forward (fused parse + verdict + rewrite) = the frame read once + the rewritten
+    header bytes of forwarded frames (0 .. l4 + 8: 42 B IPv4, 62 B IPv6) + 1 B verdict.
+    Dual-stack configs (10, 11) parse with RPKT_F_IPV6: build writes IPv6 records too,
+    forward passes RPKT_F_IPV6."""
     torch.cuda.empty_cache()
     n = args.frames or gen.DEFAULT_N[cfg]
     R = 8 if cfg == 2 else 1                  # 64-B legs: 512 MiB of frames, past the cache
@@ -849,7 +851,9 @@ def run_tx(cfg, mode, args, rank, world):
         hbs = [gen.make_batch(cfg, n, seed=gen.DEFAULT_SEED[cfg] + 7919 * rank + 104729 * r)
                for r in range(R)]
     dbs = [engine.DeviceBatch.from_host(hb) for hb in hbs]
-    recs = [engine.parse_batch(db, 3) for db in dbs]
+    pflags = gen.FLAGS.get(cfg, 3) | 3         # dual-stack configs: IPv6 records too
+    fwd_flags = pflags & F_IPV6                # forward: IPv6 frames too (rpkt_fwd_t.flags)
+    recs = [engine.parse_batch(db, pflags) for db in dbs]
     # optsc: the option walks located by compact records (rpkt_gpu_options_batch_compact)
     recs16 = [engine.parse_batch_compact(db, 3) for db in dbs] if mode == "optsc" else None
     outs = [torch.empty(hb.n * (64 if mode in ("opts", "optsc", "layers") else 1), dtype=torch.uint8,
@@ -878,7 +882,8 @@ def run_tx(cfg, mode, args, rank, world):
             engine.fields_batch(dbs[j], lays[j], reqs, values=vals[j], present=pres[j],
                                 stream=stream)
         else:
-            engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream)
+            engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream,
+                                 flags=fwd_flags)
 
     k, t_w = 0, time.perf_counter()
     while k < args.warmup or time.perf_counter() - t_w < args.min_warmup_s:
@@ -899,7 +904,12 @@ def run_tx(cfg, mode, args, rank, world):
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     r = as_records(recs[0].cpu().numpy())
     lens = hbs[0].lens()
-    fixed = r["l4_off"].astype(np.int64) + np.where(r["ip_protocol"] == 17, 8, 20)
+    # header bytes the build writes: link + IPv4 header (or the IPv6 header's first 8
+    # bytes) + the fixed L4 header
+    six = is_ip6(r)
+    l4fix = np.where(r["ip_protocol"] == 17, 8, 20)
+    fixed = np.where(six, r["l3_off"].astype(np.int64) + 8 + l4fix,
+                     r["l4_off"].astype(np.int64) + l4fix)
     floor = None                               # the 128-B line floor of the reads + writes
     fo = hbs[0].offsets[:-1].astype(np.int64) if hbs[0].offsets is not None else \
         np.arange(hbs[0].n, dtype=np.int64) * hbs[0].stride
@@ -938,15 +948,21 @@ def run_tx(cfg, mode, args, rank, world):
         tcp = (r["status"] == 0) & (r["ip_protocol"] == 6)
         l3, l4 = r["l3_off"].astype(np.int64), r["l4_off"].astype(np.int64)
         po = r["payload_off"].astype(np.int64)
-        slices = np.where(ip_parsed, l4 - l3 - 20, 0) + np.where(tcp, po - l4 - 20, 0)
+        # Ipv6OptionsIter: the extension chain [l3 + 40, l4) of an IPv6 record is walked
+        ip6_walked = is_ip6(r) & (l4 >= l3 + 40) & (r["status"] != 14) & (r["status"] != 15)
+        slices = np.where(ip_parsed, l4 - l3 - 20, 0) + np.where(tcp, po - l4 - 20, 0) + \
+            np.where(ip6_walked, l4 - l3 - 40, 0)
         fixed_io = hbs[0].n * ((REC16_BYTES if mode == "optsc" else REC_BYTES) + 64)
         alg = fixed_io + int(slices.sum())
         floor = fixed_io + line_floor(
-            np.concatenate([np.where(ip_parsed, fo + l3 + 20, 0), np.where(tcp, fo + l4 + 20, 0)]),
-            np.concatenate([np.where(ip_parsed, fo + l4, 0), np.where(tcp, fo + po, 0)]))
+            np.concatenate([np.where(ip_parsed, fo + l3 + 20, 0), np.where(tcp, fo + l4 + 20, 0),
+                            np.where(ip6_walked, fo + l3 + 40, 0)]),
+            np.concatenate([np.where(ip_parsed, fo + l4, 0), np.where(tcp, fo + po, 0),
+                            np.where(ip6_walked, fo + l4, 0)]))
     else:
         kept = outs[0].cpu().numpy().astype(bool)
-        alg = int(lens.sum()) + hbs[0].n + int(kept.sum()) * 42
+        # rewritten bytes of a kept frame: 0 .. l4 + 8 (IPv4: 42; IPv6: 62 and up)
+        alg = int(lens.sum()) + hbs[0].n + int((r["l4_off"][kept].astype(np.int64) + 8).sum())
     achieved = alg / (kern_ms / 1e3) / 1e9
     traffic, tsrc = pmc_traffic_tx("%s%d" % (mode, cfg))      # the bench leg's name
     return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
@@ -1047,14 +1063,14 @@ def headline_line(main_res, extra, args, world, engine_build, detail_path):
     }
     for k in FLOW_KEYS:
         if k in main_res:
-            line[k] = main_res[k]
+            line[k] = _r(main_res[k], 5)
     if "copy_ceiling" in main_res:
         line["copy_ceiling_gb_per_s"] = {k: v.get("gb_per_s") for k, v in
                                          main_res["copy_ceiling"].items() if isinstance(v, dict)}
     # flow-reduce fields of an extra config-4 leg at the top level too (the N-rank check)
     for k in FLOW_KEYS:
         if k not in line and "config4" in extra and k in extra["config4"]:
-            line[k] = extra["config4"][k]
+            line[k] = _r(extra["config4"][k], 5)
     line["extra"] = {k: leg_summary(v) for k, v in extra.items()}
     if len(json.dumps(line)) >= LINE_MAX:
         line["extra"] = {k: (s.get("frac") if "frac" in s else s.get("mpps"))
@@ -1078,7 +1094,8 @@ def write_detail(path, main_res, extra, args, world, engine_build):
 # legs run by default at N = 1, and at N > 1 unless --all-legs (the N-rank job stays short:
 # the headline, config 4's sharded parse + counter reduce, and the strong-scaling legs)
 LEG_DEFAULTS = {"also": ("3,4,5,7,10,11", "4"),
-                "tx": ("build2,build3,forward2,opts5,optsc5,layers9,fields9", ""),
+                "tx": ("build2,build3,build11,forward2,forward10,opts5,optsc5,opts11,layers9,"
+                       "fields9", ""),
                 "compact": ("2,3", ""), "strong": ("2,3", "2,3"), "opts": ("5", ""),
                 "ring": ("2,10", "")}
 

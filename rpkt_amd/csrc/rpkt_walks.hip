@@ -176,6 +176,13 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 #ifndef RPKT_LAY_HALF
 #define RPKT_LAY_HALF 0          // 1: refills fetch the slot's first half, the rest on demand
 #endif
+// A wave takes new frames once RPKT_LAY_TAKE_MIN of its walks ended (or none is still
+// walking); ended lanes wait until then.  Same process, byte-identical, vs taking at every
+// ended walk (1): capture mix 58.1 -> 57.2 us, config 2 43.2 -> 43.1, config 5 313.3 ->
+// 304.5 (16); 8 and 32 in between (profiles/r05_lay_take/).
+#ifndef RPKT_LAY_TAKE_MIN
+#define RPKT_LAY_TAKE_MIN 16
+#endif
 #ifndef RPKT_LAY_STAGE_MIN
 #define RPKT_LAY_STAGE_MIN 16    // ... when at least this many walks of the wave end together
 #endif
@@ -789,9 +796,16 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
             g = nx;
             H = H2;
         }
-        // lanes whose walk ended store their record and move to their next frame
+        // lanes whose walk ended store their record and move to their next frame: at once
+        // (RPKT_LAY_TAKE_MIN 1), or when enough of them ended to share the take path's
+        // fixed cost (the ended ones wait with pend set, as after an Ethernet-only walk)
         const uint64_t sm = __ballot(stop != 0);
-        if (sm) {
+        bool take = sm != 0;
+        if constexpr (RPKT_LAY_TAKE_MIN > 1)
+            take = take && ((uint32_t)__builtin_popcountll(sm) >= (uint32_t)RPKT_LAY_TAKE_MIN ||
+                            __ballot(active && stop == 0) == 0);
+        if (!take) pend = stop;
+        if (take) {
             // DYN: the wave's 64 F frames are a pool; a lane that ends a frame takes
             // the next untaken one (rank among this step's finishers), so lanes stay
             // busy until the pool is empty instead of after their own F frames
