@@ -183,3 +183,22 @@ def test_forward_ip6_fixtures_every_alignment(torch, lead):
     names = sorted(f for f in os.listdir(PKTS) if f.endswith(".dat"))
     hb = host_batch([oracle.load_dat(os.path.join(PKTS, f)) for f in names], lead)
     check_forward(torch, hb, F_IPV6)
+
+
+@pytest.mark.parametrize("stride,flen", [(64, 64), (64, 62), (48, 48), (80, 64), (96, 96)])
+def test_tx_ip6_short_strided_frames(torch, stride, flen):
+    """Dual-stack fuzz frames cut to flen bytes at `stride` (the 64-B-window compile takes
+    frame + phase <= 64): IPv6 records built and IPv6 frames forwarded as the oracle does,
+    no byte outside a frame touched."""
+    src = gen.make_batch(12, 20000, seed=stride * 7 + flen)
+    lens = src.lens()
+    buf = np.zeros(src.n * stride + 64, dtype=np.uint8)
+    for i in range(src.n):
+        a = int(src.offsets[i])
+        k = min(int(lens[i]), flen)
+        buf[i * stride:i * stride + k] = src.frames[a:a + k]
+    hb = gen.HostBatch(12, src.n, 0, buf, None, stride, flen)
+    recs = oracle_recs(hb)
+    for flags in (1, 3):
+        check_build(torch, hb, recs, flags)
+    check_forward(torch, hb, F_IPV6)
