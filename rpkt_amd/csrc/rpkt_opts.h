@@ -161,15 +161,37 @@ __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto,
     return S;
 }
 
-__device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t fb, uint32_t fo,
-                                             uint32_t l3, uint32_t l4, uint32_t* row) {
-    uint32_t nh = (gdword(rs, fb, fo + l3 + 4u) >> 16) & 0xffu;   // next_header, byte 6
+// Frame bytes [x, x + 4) of a lane's frame as a little-endian dword for the IPv6 option
+// walk: from the lane's LDS slot when they lie in the frame range [lo, hi) the slot holds
+// (frame byte x at slot[x + bias]), else from global memory.  An empty range (lo == hi)
+// reads everything from memory.
+struct OptDw {
+    const uint8_t* slot;
+    uint32_t bias, lo, hi, fo, fb;
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ uint32_t operator()(uint32_t x) const {
+        if (x >= lo && x + 4u <= hi) {
+            const uint32_t y = x + bias, a = y & ~3u;
+            return align_bytes(lds32(slot, a + 4u), lds32(slot, a), y & 3u);
+        }
+        return gdword(rs, fb, fo + x);
+    }
+};
+
+// The IPv6 half of a frame's rpkt_opts_t (Ipv6OptionsIter over every HopByHop /
+// DestOptions header of [l3 + 40, l4)): words 7..10, the trace (14, 15) and byte 27.
+struct Ip6Opts {
+    uint32_t w7, w8, w9, w10, tr_lo, tr_hi, end;
+};
+
+__device__ __forceinline__ Ip6Opts ip6_walk(const OptDw& dw, uint32_t l3, uint32_t l4) {
+    uint32_t nh = (dw(l3 + 4u) >> 16) & 0xffu;                    // next_header, byte 6
     uint32_t c = l3 + 40u;
     uint32_t cnt = 0, kinds = 0, stop = RPKT_OPT_NONE, end = 0, ra = 0, gt = 0, gl = 0, gd = 0;
     uint32_t nhdr = 0, first = 0;
     uint64_t trace = 0;
     for (int k = 0; k < RPKT_MAX_IP6_EXT && c < l4; ++k) {
-        const uint32_t d0 = gdword(rs, fb, fo + c);
+        const uint32_t d0 = dw(c);
         const uint32_t b1 = (d0 >> 8) & 0xffu;
         const uint32_t hl = nh == 44u ? 8u : (nh == 51u ? b1 * 4u + 8u : b1 * 8u + 8u);
         if (nh == 0u || nh == 60u) {
@@ -179,7 +201,7 @@ __device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t
             const uint32_t s0 = c + 2u, nb = hl - 2u;
             uint32_t pos = 0;
             while (pos < nb) {
-                const uint32_t d = gdword(rs, fb, fo + s0 + pos);
+                const uint32_t d = dw(s0 + pos);
                 const uint32_t t = d & 0xffu, rem = nb - pos;
                 if (t == 0u) {                          // a run of Pad0 (up to 4 bytes)
                     uint32_t kz = d ? (uint32_t)__builtin_ctz(d) >> 3 : 4u;
@@ -202,7 +224,7 @@ __device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t
                 if (kind == 3u) {                                        // Generic: type_,
                     gt = t;                                              // data length, the
                     gl = ln - 2u;                                        // slice's first bytes
-                    const uint32_t v = bswap32(gdword(rs, fb, fo + s0 + pos + 2u));
+                    const uint32_t v = bswap32(dw(s0 + pos + 2u));
                     gd = gl >= 4u ? v : v & ~(0xffffffffu >> (8u * gl));
                 }
                 kinds |= 1u << kind;
@@ -216,14 +238,16 @@ __device__ __forceinline__ void ip6_walk_row(__amdgpu_buffer_rsrc_t rs, uint32_t
         nh = d0 & 0xffu;
         c += hl;
     }
-    row[7] = (cnt & 0xffu) | (stop << 8) | (kinds << 16);
-    row[8] = ra | (gt << 16) | (gl << 24);
-    row[9] = nhdr | (first << 8);
-    row[10] = gd;
-    row[11] = 0u;
-    row[14] = (uint32_t)trace;
-    row[15] = (uint32_t)(trace >> 32);
-    reinterpret_cast<uint8_t*>(row)[27] = (uint8_t)end;
+    return Ip6Opts{(cnt & 0xffu) | (stop << 8) | (kinds << 16), ra | (gt << 16) | (gl << 24),
+                   nhdr | (first << 8), gd, (uint32_t)trace, (uint32_t)(trace >> 32), end};
+}
+
+// The IPv6 walks of the wave's IPv6 frames, while their windows are still in LDS (before
+// the rows are staged over them); a frame's bytes outside the window come from memory.
+__device__ __forceinline__ Ip6Opts ip6_walks(const OptSlices& S, const OptDw& dw) {
+    Ip6Opts v{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (__ballot(S.ip6) != 0 && S.ip6) v = ip6_walk(dw, S.l3, S.l4);
+    return v;
 }
 
 // The two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
@@ -313,11 +337,20 @@ __device__ __forceinline__ void walk_options(const OptWin& s, const OptSlices& S
 // The IPv6 half of one frame's row staged in LDS (`row`, 17-dword stride), for lanes whose
 // frame is IPv6; the wave synchronises before and after (other lanes wrote the rows).
 __device__ __forceinline__ void ip6_patch_rows(uint32_t* st, int lane, const OptSlices& S,
-                                               __amdgpu_buffer_rsrc_t rs, uint32_t fb,
-                                               uint32_t fo) {
+                                               const Ip6Opts& v) {
     if (__ballot(S.ip6) == 0) return;                          // wave-uniform
     wave_sync();
-    if (S.ip6) ip6_walk_row(rs, fb, fo, S.l3, S.l4, st + lane * 17);
+    if (S.ip6) {
+        uint32_t* row = st + lane * 17;
+        row[7] = v.w7;
+        row[8] = v.w8;
+        row[9] = v.w9;
+        row[10] = v.w10;
+        row[11] = 0u;
+        row[14] = v.tr_lo;
+        row[15] = v.tr_hi;
+        reinterpret_cast<uint8_t*>(row)[27] = (uint8_t)v.end;
+    }
     wave_sync();
 }
 
@@ -362,8 +395,7 @@ struct OptCur {
 __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint32_t slot_bias,
                                                     const OptSlices& S, const uint8_t* rules,
                                                     rpkt_opts_t* opts, uint32_t p0, uint32_t n,
-                                                    __amdgpu_buffer_rsrc_t rs, uint32_t fb,
-                                                    uint32_t fo) {
+                                                    const OptDw& d6) {
     // (a lane past the batch end may hold a zero record: status OK, l4 = 0, so a slice
     // can come out "negative"; it is empty, as walk_options' `on` flags treat it)
     const uint32_t t_nb = S.tcp && S.t_hi > S.t_lo ? S.t_hi - S.t_lo : 0u;
@@ -661,6 +693,8 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
         }
     }
 #endif  // RPKT_OPT_DEFER
+    // IPv6 frames' option walks, over the windows before the rows are staged on them
+    const Ip6Opts v6 = ip6_walks(S, d6);
     // rows: this frame's TCP words, then frame q's IPv4 words (word 6's top byte last)
     wave_sync();                                               // every walk has ended
     uint32_t* st = reinterpret_cast<uint32_t*>(win);
@@ -672,7 +706,7 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
     pq[14] = o[14]; pq[15] = o[15];
     reinterpret_cast<uint8_t*>(pq)[27] = (uint8_t)ip_end;
     wave_sync();
-    ip6_patch_rows(st, lane, S, rs, fb, fo);                   // IPv6 frames' option walks
+    ip6_patch_rows(st, lane, S, v6);                           // IPv6 frames' option walks
     const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
 #pragma unroll
@@ -688,13 +722,13 @@ __device__ __forceinline__ void walk_options_paired(uint8_t* win, int lane, uint
 // read by any lane of the wave after this call begins until it returns.
 __device__ __forceinline__ void store_opts(uint32_t* st, int lane, const uint32_t (&o)[16],
                                            rpkt_opts_t* opts, uint32_t p0, uint32_t n,
-                                           const OptSlices& S, __amdgpu_buffer_rsrc_t rs,
-                                           uint32_t fb, uint32_t fo) {
+                                           const OptSlices& S, const OptDw& d6) {
+    const Ip6Opts v6 = ip6_walks(S, d6);
     wave_sync();
 #pragma unroll
     for (int k = 0; k < 16; ++k) st[lane * 17 + k] = o[k];
     wave_sync();
-    ip6_patch_rows(st, lane, S, rs, fb, fo);
+    ip6_patch_rows(st, lane, S, v6);
     const uint32_t nrow = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
     u32x4* out = reinterpret_cast<u32x4*>(opts + p0);
 #pragma unroll

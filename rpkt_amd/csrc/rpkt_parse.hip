@@ -59,16 +59,26 @@ __device__ __forceinline__ void options_from_window(WaveScratch& W, __amdgpu_buf
         wave_sync();
         if (over) bias = ((fr.off + S.need_lo) & 15u) - S.need_lo;
     }
+    // the frame bytes the slot holds, for the IPv6 option walk (ip6_walk): the header
+    // window [0, kWin - ph), or a refilled slot's loaded chunks from need_lo's phase
+    uint32_t wlo = 0u, whi = (uint32_t)kWin - ph;
+    if (over) {
+        const uint32_t ph2 = (fr.off + S.need_lo) & 15u;
+        const uint32_t span = (S.need_hi - S.need_lo + ph2 + 15u) & ~15u;
+        wlo = S.need_lo - ph2;
+        whi = wlo + (span < (uint32_t)kWin ? span : (uint32_t)kWin);
+    }
+    const OptDw d6{&W.win[lane * kSlot], bias, wlo, whi, fr.off, fb, rs};
 #if RPKT_OPT_ABLATE == 1
     uint32_t o[16] = {};
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, d6);
 #elif RPKT_OPT_PAIRED
-    walk_options_paired(W.win, lane, lane * kSlot + bias, S, rules, opts, p0, n, rs, fb, fr.off);
+    walk_options_paired(W.win, lane, lane * kSlot + bias, S, rules, opts, p0, n, d6);
 #else
     const OptWin s{&W.win[lane * kSlot], bias};
     uint32_t o[16];
     walk_options(s, S, rules, o);
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, d6);
 #endif
 }
 

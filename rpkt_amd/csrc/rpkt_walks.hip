@@ -98,8 +98,19 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         doff4 = ((w14 >> 12) & 0xfu) * 4u;
     }
     const OptSlices S = opt_slices(status, proto, l3, l4, doff4, is6);
-    const uint32_t need_lo = S.need_lo, need_hi = S.need_hi;
-    const bool need = S.need;
+    // the window: the option slices; for an IPv6 record, from its next_header dword
+    // (l3 + 4) through the extension chain when the chain and the TCP slice fit in it
+    // together, so that Ipv6OptionsIter reads LDS instead of memory (ip6_walk, OptDw)
+    uint32_t need_lo = S.need_lo, need_hi = S.need_hi;
+    bool need = S.need;
+    if (S.ip6 && S.l4 > S.l3 + 40u) {
+        const uint32_t lo6 = S.l3 + 4u, hi6 = S.need && S.need_hi > S.l4 ? S.need_hi : S.l4;
+        if (hi6 - lo6 + ((fr.off + lo6) & 15u) + 16u <= (uint32_t)(kOptChunks * 16)) {
+            need_lo = lo6;
+            need_hi = hi6;
+            need = true;
+        }
+    }
 
     // window chunks that overlap the option bytes -> LDS slots
     {
@@ -133,14 +144,19 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     }
     wave_sync();
 
+    // the frame bytes the slot holds: the loaded chunks from the 16-B phase of need_lo
+    const uint32_t phw = (fr.off + need_lo) & 15u;
+    const uint32_t wspan = (need_hi - need_lo + phw + 15u) & ~15u;
+    const OptDw d6{&W.win[lane * kOptSlot], phw - need_lo, need ? need_lo - phw : 0u,
+                   need ? need_lo - phw + (wspan < kOptChunks * 16u ? wspan : kOptChunks * 16u) : 0u,
+                   fr.off, fb, rs};
 #if RPKT_OPT_PAIRED
-    walk_options_paired(W.win, lane, lane * kOptSlot + (((fr.off + need_lo) & 15u) - need_lo), S,
-                        rules, opts, p0, n, rs, fb, fr.off);
+    walk_options_paired(W.win, lane, lane * kOptSlot + (phw - need_lo), S, rules, opts, p0, n, d6);
 #else
-    const OptWin s{&W.win[lane * kOptSlot], ((fr.off + need_lo) & 15u) - need_lo};
+    const OptWin s{&W.win[lane * kOptSlot], phw - need_lo};
     uint32_t o[16];
     walk_options(s, S, rules, o);
-    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, rs, fb, fr.off);
+    store_opts(reinterpret_cast<uint32_t*>(W.win), lane, o, opts, p0, n, S, d6);
 #endif
 }
 
