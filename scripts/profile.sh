@@ -8,7 +8,7 @@ TAG=$1; CFG=$2
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS=(--no-cpu --config "$CFG" --also "" --tx "" --compact "" --strong "" --opts "" --host "" --rx-graph "" --steps 20 --warmup 5 "${@:3}")
+ARGS=(--no-cpu --config "$CFG" --also "" --tx "" --compact "" --strong "" --opts "" --ring "" --host "" --rx-graph "" --steps 20 --warmup 5 "${@:3}")
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT" -o trace \
     -- python3 "$R/bench.py" "${ARGS[@]}" > "$OUT/trace_bench.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT" -o fetch \
