@@ -26,7 +26,13 @@ rank; otherwise `--gpus N` (N > 1) starts the N rank processes itself, before an
 call, and exits with their status.  Batches are independent, so ranks never exchange
 frames (weak scaling for configs 2/3); config 4 shards one batch and sums its flow
 counters with rpkt_gpu_flow_reduce (RCCL).  The timed region is bracketed by
-barrier + synchronize and the max over ranks is reported.
+barrier + synchronize and the max over ranks is reported.  At N > 1 the default legs are
+the headline, config 4 and the strong-scaling legs only (LEG_DEFAULTS, --all-legs).
+
+Output: rank 0 prints ONE compact JSON line (< 8,000 bytes: the contract keys, the main
+leg's roofline and CPU baseline, per extra leg its kernel/step times, roofline fraction
+and traffic ratio) and writes every leg's full result to --detail
+(gpurun_out/bench_detail.json), whose path the line gives.
 """
 import argparse
 import ctypes
@@ -1129,8 +1135,9 @@ def main():
     ap.add_argument("--min-warmup-s", type=float, default=0.3,
                     help="extend the W warmup steps to at least this much GPU time")
     ap.add_argument("--reduce-comm", default="auto", choices=["own", "auto", "torch"],
-                    help="flow-counter reduce: rpkt_gpu_flow_reduce on the library's own RCCL "
-                         "communicator (own), on torch's (auto), or torch's all_reduce (torch)")
+                    help="flow-counter reduce: rpkt_gpu_flow_reduce on torch's RCCL communicator "
+                         "(auto, the default), on the library's own, joined with a deadline "
+                         "(own), or torch's all_reduce (torch)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
