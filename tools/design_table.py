@@ -1,7 +1,8 @@
-"""Regenerate DESIGN.md §5's roofline table from a bench line and the committed PMC
-traffic summaries (profiles/traffic_*.json).  Host side.
+"""Regenerate DESIGN.md §6's roofline table from a bench detail file (bench.py --detail,
+every leg's full result) and the committed PMC traffic summaries
+(profiles/traffic_*.json).  Host side.
 
-Usage: python tools/design_table.py profiles/r03_bench_final.json
+Usage: python tools/design_table.py profiles/r05_bench_detail.json [--print]
 """
 import json
 import os
@@ -10,67 +11,88 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def rw(name, leg=None):
-    t = json.load(open(os.path.join(ROOT, "profiles", name + ".json")))
+def traffic(name, leg=None):
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", name + ".json")))
+    except OSError:
+        return None
     if leg:
-        t = t["legs"][leg]
-    return t["hbm_read_bytes_corrected"], t["hbm_write_bytes"]
+        t = t["legs"].get(leg)
+        if t is None:
+            return None
+    return t["traffic_bytes_per_launch"]
 
 
-def rows(d):
-    E = d["extra"]
-    yield "**config 2**: 1M × 64 B UDP, IPv4 sum (8 rotated batches, cache-free)", d, rw("traffic_c2")
-    for key, label, tr in (
-            ("config2_compact", "config 2, compact records", "traffic_c2_compact"),
-            ("config3", "config 3: 1M × 1500 B TCP, both sums", "traffic_c3"),
-            ("config3_compact", "config 3, compact records", "traffic_c3_compact"),
-            ("config4", "config 4: 8M IMIX + flow counters (parse + histogram + slab reduce per step)",
-             "traffic_c4"),
-            ("config5", "config 5: 4M VLAN/QinQ + options", "traffic_c5"),
-            ("config5_opts", "config 5 + both option walks, fused (80-B records + 64-B walks)",
-             "traffic_c5_opts"),
-            ("config5_opts_compact", "config 5 + both option walks, fused, compact records",
-             "traffic_c5_opts_compact"),
-            ("config7", "config 7: 256K × 8000 B jumbo mbuf chains", "traffic_c7")):
-        yield label, E[key], rw(tr)
-    for key, label in (
-            ("build2", "TX build 2: 1M × 64 B, both sums filled (8 rotated batches)"),
-            ("build3", "TX build 3: 1M × 1500 B, both sums filled"),
-            ("forward2", "forward 2: 1M × 64 B loopback_rx (8 rotated batches)"),
-            ("opts5", "options 5: 4M frames with options (standalone walk)"),
-            ("optsc5", "options 5 from compact records"),
-            ("layers9", "layers 9: 1M frames, capture mix"),
-            ("fields9", "fields 9: 1M frames × 16 getters, capture mix")):
-        yield label, E["tx_" + key], rw("traffic_tx", key)
+# (label, leg key in the detail file, traffic summary, traffic leg)
+ROWS = [
+    ("**config 2**: 1M × 64 B, IPv4 sum (headline)", "main", "traffic_c2", None),
+    ("config 2, 8 batches per `parse_ring` launch", "config2_ring8", None, None),
+    ("config 2, compact records", "config2_compact", "traffic_c2_compact", None),
+    ("config 2 ring, compact", "config2_ring8_compact", None, None),
+    ("config 3: 1M × 1500 B TCP, both sums", "config3", "traffic_c3", None),
+    ("config 3, compact records", "config3_compact", "traffic_c3_compact", None),
+    ("config 4: 8M IMIX + flow counters", "config4", "traffic_c4", None),
+    ("config 5: 4M VLAN/QinQ + IPv4/TCP options", "config5", "traffic_c5", None),
+    ("config 5 + fused option walks", "config5_opts", "traffic_c5_opts", None),
+    ("config 7: 256K × 8000 B mbuf chains", "config7", "traffic_c7", None),
+    ("**config 11**: 1M × 1500 B dual stack (IPv6 0–3 ext. headers), both sums", "config11",
+     "traffic_c11", None),
+    ("config 10: 1M × 64 B dual stack UDP, both sums", "config10", "traffic_c10", None),
+    ("config 10, 8 batches per `parse_ring` launch", "config10_ring8", None, None),
+    ("TX build 2 / build 3", ("tx_build2", "tx_build3"), "traffic_tx", ("build2", "build3")),
+    ("TX build 11 (dual stack, IPv6 records built)", "tx_build11", "traffic_tx", "build11"),
+    ("forward 2 / forward 10 (dual stack, `RPKT_F_IPV6`)", ("tx_forward2", "tx_forward10"),
+     "traffic_tx", ("forward2", "forward10")),
+    ("options 5 standalone (80-B / 16-B records)", ("tx_opts5", "tx_optsc5"), "traffic_tx",
+     ("opts5", "optsc5")),
+    ("options 11 standalone (TCP + `Ipv6OptionsIter`)", "tx_opts11", "traffic_tx", "opts11"),
+    ("layers 9 (capture mix)", "tx_layers9", "traffic_tx", "layers9"),
+    ("fields 9 (16 getters)", "tx_fields9", "traffic_tx", "fields9"),
+]
 
 
-def fmt(x):
+def fmt_bytes(x):
     return "%.1f MB" % (x / 1e6) if x < 1e9 else "%.3f GB" % (x / 1e9)
+
+
+def cell(legs, f, sep=" / "):
+    return sep.join(f(x) for x in legs)
 
 
 def table(d):
     out = []
-    for name, leg, (rd, wr) in rows(d):
-        r, ms = leg["roofline"], leg["kernel_ms"]
-        alg = r["alg_bytes_per_launch"]
-        frac = ("**%.2f**" if name.startswith("**") else "%.2f") % r["frac"]
-        out.append("| %s | %s | %.1f µs | %.2f TB/s | %s | %s (%s + %s)%s |" % (
-            name, fmt(alg), ms * 1e3, alg / (ms * 1e-3) / 1e12, frac, fmt(rd + wr), fmt(rd),
-            fmt(wr), "‡" if name.startswith("options") else ""))
+    for label, key, tname, tleg in ROWS:
+        keys = key if isinstance(key, tuple) else (key,)
+        tlegs = tleg if isinstance(tleg, tuple) else (tleg,) * len(keys)
+        legs = [d["main"] if k == "main" else d["extra"].get(k) for k in keys]
+        if any(v is None for v in legs):
+            continue
+        alg = [v["roofline"]["alg_bytes_per_launch"] for v in legs]
+        ms = [v["kernel_ms"] for v in legs]
+        frac = [v["roofline"]["frac"] for v in legs]
+        tr = [traffic(tname, tl) if tname else None for tl in tlegs]
+        ratio = cell([t / a if t else None for t, a in zip(tr, alg)],
+                     lambda x: "—" if x is None else "%.3f" % x)
+        bold = label.startswith("**")
+        fr = cell(frac, lambda x: ("**%.2f**" if bold else "%.2f") % x)
+        out.append("| %s | %s | %s | %s | %s |" % (
+            label, cell(alg, fmt_bytes), cell(ms, lambda x: "%.1f µs" % (x * 1e3)), fr, ratio))
     return out
 
 
-def main(path):
+def main(path, print_only=False):
     d = json.load(open(path))
-    p = os.path.join(ROOT, "DESIGN.md")
-    s = open(p).read()
-    i = s.index("| leg | alg. bytes / launch |")
-    j = s.index("\n\n", i)
-    hdr = s[i:s.index("\n", s.index("\n", i) + 1) + 1]
-    s = s[:i] + hdr + "\n".join(table(d)) + s[j:]
-    open(p, "w").write(s)
-    print("\n".join(table(d)))
+    rows = table(d)
+    if not print_only:
+        p = os.path.join(ROOT, "DESIGN.md")
+        s = open(p).read()
+        i = s.index("| leg | alg. bytes / launch |")
+        j = s.index("\n\n", i)
+        hdr = s[i:s.index("\n", s.index("\n", i) + 1) + 1]
+        s = s[:i] + hdr + "\n".join(rows) + s[j:]
+        open(p, "w").write(s)
+    print("\n".join(rows))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], "--print" in sys.argv[2:])
