@@ -202,3 +202,29 @@ def test_tx_ip6_short_strided_frames(torch, stride, flen):
     for flags in (1, 3):
         check_build(torch, hb, recs, flags)
     check_forward(torch, hb, F_IPV6)
+
+
+def test_build_from_host_build_views(torch):
+    """Records composed by the host-side build views (rpkt_amd/txviews.py: rpkt's
+    prepend_header + setters) for the reference's captures, its loopback_tx frames and a
+    QinQ/IPv6/routing/TCP-options chain, built by rpkt_gpu_build_batch with and without the
+    checksum fill: the same bytes as the oracle build."""
+    import test_txviews as tt
+    from rpkt_amd import txviews as tv
+    chains, lens, pays = [], [], []
+    for name in sorted(f for f in os.listdir(PKTS) if f.endswith(".dat")):
+        f = bytes(oracle.load_dat(os.path.join(PKTS, name)))
+        r = oracle.parse_one(f, F6)
+        if r["status"] != STATUS["OK"] or int(r["ip_protocol"]) not in (6, 17):
+            continue
+        chains.append(tt.chain_from_capture(f, r))
+        lens.append(len(f))
+        pays.append(f[int(r["payload_off"]):])
+    for k in range(200):
+        chains.append(tt.loopback_tx_chain("172.74.%d.%d" % (2 + k // 250, 2 + k % 250)))
+        lens.append(1500)
+        pays.append(b"\xae" * 1458)
+    buf, offs, recs = tv.assemble(chains, lens, pays)
+    hb = gen.HostBatch(0, len(lens), 0, buf, offs, 0, 0)
+    for flags in (0, 3):
+        check_build(torch, hb, recs, flags)
