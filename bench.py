@@ -123,7 +123,17 @@ def usable_cpus():
     return n
 
 
-def launch_ranks(n, argv):
+def share_gpu_env(rank):
+    """--share-gpu: RCCL refuses two ranks of one host on one device ("Duplicate GPU
+    detected"); a distinct NCCL_HOSTID per rank makes the ranks look like separate hosts,
+    which then talk over the socket transport on loopback.  A one-GPU rehearsal of the
+    cross-rank RCCL code (communicators, the C ABI all-reduce, torch's ProcessGroupNCCL),
+    not an xGMI measurement."""
+    return {"NCCL_HOSTID": "rpkt-share-%d" % rank, "NCCL_SOCKET_IFNAME": "lo",
+            "NCCL_IB_DISABLE": "1"}
+
+
+def launch_ranks(n, argv, share=False):
     """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE + a local
     rendezvous), wait for all of them and return the worst exit status.  Runs before
     anything touches the GPU; the ranks are children, never an exec of this process."""
@@ -135,6 +145,8 @@ def launch_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if share:
+            env.update(share_gpu_env(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
                                       env=env))
     rc = 0
@@ -1059,7 +1071,8 @@ def headline_line(main_res, extra, args, world, engine_build, detail_path):
                    "layout": main_res["layout"], "checksums": main_res["flags"],
                    "parallelism": "replicas x%d (independent batches, no collective)" % world
                    if args.config != 4 else "shard x%d + RCCL all-reduce" % world,
-                   "dist_backend": args.dist_backend if world > 1 else None},
+                   "dist_backend": args.dist_backend if world > 1 else None,
+                   "shared_gpu": bool(args.share_gpu) if world > 1 else None},
         "frame_gb_per_s": round(main_res["frame_gb_per_s"], 2),
         "kernel_ms": round(main_res["kernel_ms"], 5),
         "engine_build": engine_build,
@@ -1140,6 +1153,9 @@ def main():
                          "(own), or torch's all_reduce (torch)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearse N nccl ranks on fewer GPUs (rank r on cuda:r %% ndev; a "
+                         "distinct NCCL_HOSTID per rank, RCCL over loopback sockets)")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 CPU leg")
     ap.add_argument("--record", default="full", choices=["full", "compact"],
                     help="record size of the main leg (profiling the compact kernel alone)")
@@ -1171,19 +1187,23 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: start the N ranks here (before any GPU call) and wait for them
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], share=args.share_gpu))
     rank, local, world = dist_env()
+    if args.share_gpu and args.dist_backend == "nccl":
+        for k, v in share_gpu_env(rank).items():      # read by RCCL at communicator init
+            os.environ.setdefault(k, v)
     if world != args.gpus:
         print("[bench] error: %d rank(s) launched for --gpus %d" % (world, args.gpus),
               file=sys.stderr)
         sys.exit(3)
     ndev = torch.cuda.device_count()                 # counts without initialising HIP
-    if args.dist_backend == "nccl" and local >= ndev:
+    shared = args.dist_backend == "gloo" or args.share_gpu
+    if args.dist_backend == "nccl" and local >= ndev and not args.share_gpu:
         print("[bench] error: rank %d needs cuda:%d but %d GPU(s) are visible (use "
               "--dist-backend gloo to rehearse ranks on one GPU)" % (rank, local, ndev),
               file=sys.stderr)
         sys.exit(3)
-    dev = local % ndev if args.dist_backend == "gloo" else local
+    dev = local % ndev if shared else local
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":

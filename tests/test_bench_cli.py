@@ -75,7 +75,7 @@ def _r04_legs():
 
 
 class _Args:
-    config, steps, warmup, dist_backend = 2, 20, 5, "nccl"
+    config, steps, warmup, dist_backend, share_gpu = 2, 20, 5, "nccl", False
 
 
 def test_headline_line_fits_the_driver_tail():

@@ -72,8 +72,9 @@ def test_ranks_hip_flow_counters_equal_whole_batch(tmp_path, world):
     assert np.array_equal(got.reshape(-1, 4), want)
 
 
-def test_bench_launches_two_ranks(tmp_path):
-    """bench.py --gpus 2 starts its own two ranks (no torchrun) and runs the N-rank default
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_n_ranks(tmp_path, world):
+    """bench.py --gpus N starts its own N ranks (no torchrun) and runs the N-rank default
     leg set (the headline, config 4's shards + counter reduce, the strong legs): the
     counter sum covers every frame of every launch of every rank and is verified against
     torch's sum, and rank 0's one stdout line parses and fits the driver's 8,000-char
@@ -81,7 +82,7 @@ def test_bench_launches_two_ranks(tmp_path):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     detail = str(tmp_path / "detail.json")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world),
                         "--dist-backend", "gloo", "--no-cpu", "--frames", "200000", "--steps",
                         "3", "--warmup", "1", "--min-warmup-s", "0", "--detail", detail],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
@@ -89,14 +90,15 @@ def test_bench_launches_two_ranks(tmp_path):
     out = r.stdout.strip().splitlines()
     assert len(out) == 1 and len(out[0]) < 8000, out
     line = json.loads(out[0])
-    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "gloo"
+    assert line["n_gpus"] == world and line["config"]["dist_backend"] == "gloo"
     assert set(line["extra"]) == {"config4", "config2_strong", "config3_strong"}
+    assert line["config"]["frames_per_rank"] == 200000 and "copy_ceiling_gb_per_s" not in line
     assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
     assert line["flow_reduce_via"] == "gloo" and line["flow_reduce_verified"] is True
     assert line["roofline"]["frac"] > 0 and line["cpu_baseline"] is None
     with open(detail) as fh:
         full = json.load(fh)
-    assert full["n_gpus"] == 2 and "roofline" in full["extra"]["config4"]
+    assert full["n_gpus"] == world and "roofline" in full["extra"]["config4"]
 
 
 RCCL_SCRIPT = r"""
@@ -238,3 +240,60 @@ def test_flow_reduce_on_the_library_own_communicator(tmp_path):
                        timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "own comm ok" in r.stdout
+
+
+def _probe(world, **env):
+    e = dict(os.environ, **{k: str(v) for k, v in env.items()})
+    e.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_share_probe.py"),
+                        str(world)], capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert sorted(x["rank"] for x in lines) == list(range(world)), lines
+    return lines
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_ranks_sharing_one_gpu(world):
+    """N RCCL ranks on the one leased GPU (a distinct NCCL_HOSTID per rank: RCCL sees N
+    hosts and talks over loopback sockets): each rank's shard of config 4 parsed and counted
+    by the HIP engine, the counters summed by rpkt_gpu_flow_reduce over ncclAllReduce on
+    torch's communicator (auto) and on the library's own, joined across the ranks with
+    rpkt_gpu_comm_init_timeout (own); both equal torch's all_reduce and cover every frame."""
+    for x in _probe(world):
+        assert x["auto"]["path"] == "rccl" and x["own"]["path"] == "rccl_own", x
+        for via in ("auto", "own"):
+            assert x[via]["pkts"] == 400000 and x[via]["equal_torch"] is True, x
+
+
+def test_own_comm_peer_never_joins_real_rccl():
+    """Rank 1 fails before joining the library's communicator: rank 0's RCCL join is
+    aborted at its 3-s deadline, the group agrees, and every rank falls back to torch's
+    communicator (path rccl) with the right sums -- no hang."""
+    lines = _probe(2, RPKT_PROBE_FAIL_RANK=1, RPKT_PROBE_TIMEOUT_MS=3000)
+    for x in lines:
+        assert x["own"]["path"] == "rccl" and x["own"]["pkts"] == 400000, x
+        assert x["own"]["equal_torch"] is True and "own communicator" in x["own"]["error"], x
+        assert x["own"]["seconds"] < 60, x
+    assert "ncclResult 7" in [x for x in lines if x["rank"] == 0][0]["own"]["error"]
+
+
+@pytest.mark.parametrize("comm", ["auto", "own"])
+def test_bench_nccl_ranks_sharing_one_gpu(tmp_path, comm):
+    """bench.py --gpus 2 --share-gpu: the N-rank default job over RCCL (nccl backend) on
+    the one GPU, both counter-reduce paths: the line parses, every counter word equals
+    torch's sum, and the frame total covers every launch of every rank."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--share-gpu", "--reduce-comm", comm, "--no-cpu", "--frames", "200000",
+                        "--steps", "3", "--warmup", "1", "--min-warmup-s", "0", "--detail",
+                        str(tmp_path / "d.json")], capture_output=True, text=True, timeout=300,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "nccl"
+    assert line["config"]["shared_gpu"] is True
+    assert line["flow_reduce_via"] == ("rccl_own" if comm == "own" else "rccl"), line
+    assert line["flow_reduce_verified"] is True
+    assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
