@@ -1189,6 +1189,12 @@ def main():
         # no launcher: start the N ranks here (before any GPU call) and wait for them
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], share=args.share_gpu))
     rank, local, world = dist_env()
+    # stdout carries ONE line, the JSON result: the libraries loaded below print to fd 1
+    # (RCCL's version banner at communicator creation, gloo's peer list), so fd 1 points at
+    # stderr for the whole run and the line is written to the saved stdout at the end
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     if args.share_gpu and args.dist_backend == "nccl":
         for k, v in share_gpu_env(rank).items():      # read by RCCL at communicator init
             os.environ.setdefault(k, v)
@@ -1209,15 +1215,7 @@ def main():
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
-            # gloo announces its peers on fd 1: keep stdout to the one JSON line
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("gloo")
-            finally:
-                os.dup2(saved, 1)
-                os.close(saved)
+            dist.init_process_group("gloo")
         if dist.get_world_size() != args.gpus:
             print("[bench] error: world size %d != --gpus %d" % (dist.get_world_size(),
                                                                   args.gpus), file=sys.stderr)
@@ -1261,7 +1259,8 @@ def main():
         except OSError as e:
             detail = "not written: %s" % e
         line = headline_line(main_res, extra, args, world, build, detail)
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(line) + "\n").encode())
     # a counter sum that is wrong (not merely taken by the fallback path) fails the run
     bad_counters = any(r.get("flow_reduce_verified") is False or
                        r.get("flow_pkts_total", 0) != r.get("flow_pkts_expected", 0)

@@ -291,7 +291,9 @@ def test_bench_nccl_ranks_sharing_one_gpu(tmp_path, comm):
                         str(tmp_path / "d.json")], capture_output=True, text=True, timeout=300,
                        env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads(r.stdout.strip().splitlines()[-1])
+    out = r.stdout.strip().splitlines()
+    assert len(out) == 1, out[:8]                  # RCCL's banner goes to stderr
+    line = json.loads(out[0])
     assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "nccl"
     assert line["config"]["shared_gpu"] is True
     assert line["flow_reduce_via"] == ("rccl_own" if comm == "own" else "rccl"), line
