@@ -266,10 +266,13 @@ def fused_vs_parse(dbs, recs, obufs, flags, compact, rounds=7, k=10):
             "ratio": round(med["fused"] / med["parse"], 4), "rounds": rounds, "launches": k}
 
 
-def pmc_traffic(cfg, compact=False, opts=False):
+def pmc_traffic(cfg, compact=False, opts=False, n=None):
     """Per-launch HBM traffic of parse_kernel for this config (and record size, and the
     fused option walks) from the rocprofv3 PMC summary committed under profiles/
-    (tools/traffic.py), when it was measured on this exact engine build; else None."""
+    (tools/traffic.py), when it was measured on this exact engine build and a launch
+    covers as many frames as the profiled one; else None."""
+    if n is not None and not profiled_size(cfg, n):
+        return None, None
     path = os.path.join(ROOT, "profiles", "traffic_c%d%s%s.json" % (
         cfg, "_opts" if opts else "", "_compact" if compact else ""))
     try:
@@ -280,6 +283,13 @@ def pmc_traffic(cfg, compact=False, opts=False):
     if not same_unit(t.get("engine_build"), "parse"):
         return None, None
     return int(t["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
+def profiled_size(cfg, n):
+    """Whether a launch over n frames of config cfg matches the committed PMC profiles:
+    they are taken by scripts/refresh_profiles.sh at N=1 with the default frame counts, so
+    an N-rank shard (config 4, the strong legs) or a --frames run gets traffic None."""
+    return n == gen.DEFAULT_N[cfg]
 
 
 def same_unit(profiled_build, unit):
@@ -297,9 +307,12 @@ def same_unit(profiled_build, unit):
     return h is not None and h == unit_hash(profiled_build)
 
 
-def pmc_traffic_tx(leg):
+def pmc_traffic_tx(leg, n=None):
     """Per-launch HBM traffic of a TX / walk leg (profiles/traffic_tx.json, from a
-    rocprofv3 PMC profile of those legs on this exact engine build); else None."""
+    rocprofv3 PMC profile of those legs on this exact engine build, at the profiled frame
+    count); else None."""
+    if n is not None and not profiled_size(int(leg.lstrip("abcdefghijklmnopqrstuvwxyz")), n):
+        return None, None
     path = os.path.join(ROOT, "profiles", "traffic_tx.json")
     try:
         with open(path) as fh:
@@ -527,7 +540,7 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
     mpps = frames_job * args.steps / wall / 1e6
     gbps = bytes_job * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic(cfg, compact, opts)
+    traffic, tsrc = pmc_traffic(cfg, compact, opts, hbs[0].n)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
         "warmup_launches": warm,
@@ -982,7 +995,7 @@ def run_tx(cfg, mode, args, rank, world):
         # rewritten bytes of a kept frame: 0 .. l4 + 8 (IPv4: 42; IPv6: 62 and up)
         alg = int(lens.sum()) + hbs[0].n + int((r["l4_off"][kept].astype(np.int64) + 8).sum())
     achieved = alg / (kern_ms / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic_tx("%s%d" % (mode, cfg))      # the bench leg's name
+    traffic, tsrc = pmc_traffic_tx("%s%d" % (mode, cfg), hbs[0].n)   # the bench leg's name
     return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
             "ms_per_step": wall / args.steps * 1e3, "frames_per_rank": hbs[0].n,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

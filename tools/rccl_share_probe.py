@@ -65,7 +65,9 @@ def rank_main():
     dist.barrier()
     rd.release_own_comms()
     dist.destroy_process_group()
-    print(json.dumps(out), flush=True)
+    # one write(2) per rank: print() may issue the line and its newline as two writes
+    # (unbuffered stdout), and the ranks share the pipe
+    os.write(1, (json.dumps(out) + "\n").encode())
 
 
 def main(world):
