@@ -299,3 +299,32 @@ def test_bench_nccl_ranks_sharing_one_gpu(tmp_path, comm):
     assert line["flow_reduce_via"] == ("rccl_own" if comm == "own" else "rccl"), line
     assert line["flow_reduce_verified"] is True
     assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
+
+
+def test_bench_under_torchrun_as_the_driver_launches_it(tmp_path):
+    """The driver's own N>1 launch form: python -m torch.distributed.run --nnodes=1
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P bench.py --gpus 2 ... --
+    here with --share-gpu (both ranks on the one GPU, RCCL over loopback).  bench.py must
+    take RANK / LOCAL_RANK / WORLD_SIZE from torchrun (not start ranks of its own) and print
+    exactly one stdout line, rank 0's, with the counters verified."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu",
+                        "--no-cpu", "--frames", "200000", "--steps", "3", "--warmup", "1",
+                        "--min-warmup-s", "0", "--detail", str(tmp_path / "d.json")],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = r.stdout.strip().splitlines()
+    assert len(out) == 1, out[:8]
+    line = json.loads(out[0])
+    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "nccl"
+    assert line["flow_reduce_via"] == "rccl" and line["flow_reduce_verified"] is True, line
+    assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
+    assert len(json.dumps(line)) < 8000
