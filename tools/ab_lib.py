@@ -72,7 +72,7 @@ def main():
                gen.make_batch(cfg, args.n or None, seed=gen.DEFAULT_SEED[cfg] + 104729 * r)
                for r in range(R)]
         dbs = [engine.DeviceBatch.from_host(h) for h in hbs]
-        recss = [engine.parse_batch(d, 3) for d in dbs]
+        recss = [engine.parse_batch(d, gen.FLAGS.get(cfg, 3) | 3) for d in dbs]   # as bench.py
     R = len(hbs)
     hb = hbs[0]
     descs = [d.desc() for d in dbs]
@@ -94,7 +94,7 @@ def main():
                 ctypes.byref(descs[k % R]), recss[k % R].data_ptr(), out.data_ptr(), sp))
         elif mode == "optsc":                       # option walks from compact records
             if "recs16" not in outs:
-                outs["recs16"] = [engine.parse_batch_compact(d, 3) for d in dbs]
+                outs["recs16"] = [engine.parse_batch_compact(d, gen.FLAGS.get(cfg, 3) | 3) for d in dbs]
             r16 = outs["recs16"]
             L.rpkt_gpu_options_batch_compact.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p]
