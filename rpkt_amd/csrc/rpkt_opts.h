@@ -139,7 +139,8 @@ struct OptSlices {
     bool need;
     bool ip6;                      // IPv6 header parsed: the IPv6 option walk (ip6_walk_row)
     uint32_t l3, l4;               //   over the extension chain [l3 + 40, l4)
-};
+    uint32_t nh0;                  // its first next_header (frame byte l3 + 6) when the caller
+};                                 //   has it (record word 7), else 256: read from the frame
 
 // is6: an IPv6 record (RPKT_F_IPV6): no IPv4 option slice; its TCP slice as any other
 __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto, uint32_t l3,
@@ -158,6 +159,7 @@ __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto,
     S.ip6 = is6 && status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN;
     S.l3 = l3;
     S.l4 = l4;
+    S.nh0 = 256u;
     return S;
 }
 
@@ -184,8 +186,8 @@ struct Ip6Opts {
     uint32_t w7, w8, w9, w10, tr_lo, tr_hi, end;
 };
 
-__device__ __forceinline__ Ip6Opts ip6_walk(const OptDw& dw, uint32_t l3, uint32_t l4) {
-    uint32_t nh = (dw(l3 + 4u) >> 16) & 0xffu;                    // next_header, byte 6
+__device__ __forceinline__ Ip6Opts ip6_walk(const OptDw& dw, uint32_t l3, uint32_t l4, uint32_t nh0) {
+    uint32_t nh = nh0 < 256u ? nh0 : (dw(l3 + 4u) >> 16) & 0xffu;  // next_header, byte 6
     uint32_t c = l3 + 40u;
     uint32_t cnt = 0, kinds = 0, stop = RPKT_OPT_NONE, end = 0, ra = 0, gt = 0, gl = 0, gd = 0;
     uint32_t nhdr = 0, first = 0;
@@ -246,7 +248,7 @@ __device__ __forceinline__ Ip6Opts ip6_walk(const OptDw& dw, uint32_t l3, uint32
 // the rows are staged over them); a frame's bytes outside the window come from memory.
 __device__ __forceinline__ Ip6Opts ip6_walks(const OptSlices& S, const OptDw& dw) {
     Ip6Opts v{0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (__ballot(S.ip6) != 0 && S.ip6) v = ip6_walk(dw, S.l3, S.l4);
+    if (__ballot(S.ip6) != 0 && S.ip6) v = ip6_walk(dw, S.l3, S.l4, S.nh0);
     return v;
 }
 

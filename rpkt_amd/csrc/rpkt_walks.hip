@@ -50,6 +50,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 
     // records of the tile (coalesced): status, IP protocol, l3 / l4 offsets, TCP doff
     uint32_t status, proto, l3, l4, doff4;
+    uint32_t nh0 = 256u;                                 // IPv6: the first next_header
     bool is6;                                            // an IPv6 record (RPKT_F_IPV6)
     if constexpr (C16) {
         const u32x4* in = reinterpret_cast<const u32x4*>(recs_any);
@@ -84,7 +85,7 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         wave_sync();
         const uint32_t w0 = st[lane * 21 + 0], w8 = st[lane * 21 + 8];
         const uint32_t w14 = st[lane * 21 + 14], w16 = st[lane * 21 + 16];
-        const uint32_t w5 = st[lane * 21 + 5];
+        const uint32_t w5 = st[lane * 21 + 5], w7 = st[lane * 21 + 7];
         wave_sync();
         status = w0 & 0xffu;
         // the dispatch ethertype: the outer one, or the last VLAN tag's
@@ -96,15 +97,24 @@ void options_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
         l3 = w16 & 0xffffu;
         l4 = w16 >> 16;
         doff4 = ((w14 >> 12) & 0xfu) * 4u;
+        nh0 = (w7 >> 16) & 0xffu;                        // ip6_next_header, record byte 30
     }
-    const OptSlices S = opt_slices(status, proto, l3, l4, doff4, is6);
-    // the window: the option slices; for an IPv6 record, from its next_header dword
-    // (l3 + 4) through the extension chain when the chain and the TCP slice fit in it
-    // together, so that Ipv6OptionsIter reads LDS instead of memory (ip6_walk, OptDw)
+    OptSlices S = opt_slices(status, proto, l3, l4, doff4, is6);
+    // the window: the option slices; for an IPv6 record, the extension chain [l3 + 40, l4)
+    // (and the TCP slice after it) when they fit, so that Ipv6OptionsIter reads LDS
+    // instead of memory (ip6_walk, OptDw).  The chain's first next_header (frame byte
+    // l3 + 6) comes from the 80-B record, or, with compact records, from a dword load
+    // issued with the window's.  (Round 5 started the window at l3 + 4 for that byte: 10 %
+    // of config 11's chains then missed the window, and 92 % of its waves waited on
+    // dependent global reads; from l3 + 40, 0.8 % and 18 %.)
+    if constexpr (C16) {
+        if (S.ip6 && S.l4 > S.l3 + 40u) nh0 = (gdword(rs, fb, fr.off + S.l3 + 4u) >> 16) & 0xffu;
+    }
+    S.nh0 = nh0;
     uint32_t need_lo = S.need_lo, need_hi = S.need_hi;
     bool need = S.need;
     if (S.ip6 && S.l4 > S.l3 + 40u) {
-        const uint32_t lo6 = S.l3 + 4u, hi6 = S.need && S.need_hi > S.l4 ? S.need_hi : S.l4;
+        const uint32_t lo6 = S.l3 + 40u, hi6 = S.need && S.need_hi > S.l4 ? S.need_hi : S.l4;
         if (hi6 - lo6 + ((fr.off + lo6) & 15u) + 16u <= (uint32_t)(kOptChunks * 16)) {
             need_lo = lo6;
             need_hi = hi6;
