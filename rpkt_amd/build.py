@@ -36,6 +36,14 @@ SECOND_COMPILES = [("rpkt_tx.hip", "rpkt_tx_w64.o", ["-DRPKT_WIN=64", "-DRPKT_TX
                                                            "-Wno-unused-function",
                                                            "-Wno-unused-const-variable",
                                                            "-Wno-unneeded-internal-declaration"])]
+# the csrc headers each unit includes (directly or through another header): a unit's
+# hash covers these, so a change to the option walks' header leaves tx / fields profiles valid
+UNIT_HEADERS = {"rpkt_parse.hip": ("rpkt_common.h", "rpkt_opts.h"),
+                "rpkt_tx.hip": ("rpkt_common.h",),
+                "rpkt_walks.hip": ("rpkt_common.h", "rpkt_opts.h", "rpkt_proto_table.h"),
+                "rpkt_fields.hip": ("rpkt_common.h",),
+                "rpkt_abi.hip": ("rpkt_common.h",),
+                "rpkt_coll.hip": ("rpkt_common.h",)}
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
 HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 
@@ -54,9 +62,8 @@ def source_hash(units=None):
     h = hashlib.sha1()
     srcs = GPU_SRC if units is None else [f for f in GPU_SRC if os.path.basename(f) in units]
     deps = GPU_DEPS
-    if units is not None:                  # the generated table is the walk unit's alone
-        deps = [d for d in GPU_DEPS if not d.endswith("rpkt_proto_table.h") or
-                "rpkt_walks.hip" in units]
+    if units is not None:                  # the headers those units include
+        deps = [d for d in GPU_DEPS if any(os.path.basename(d) in UNIT_HEADERS[u] for u in units)]
     for f in srcs + deps + HDR:
         with open(f, "rb") as fh:
             h.update(fh.read())

@@ -279,3 +279,25 @@ def test_fields_batch_argument_checks(L):
     b.n = 4
     assert L.rpkt_gpu_fields_batch(ctypes.byref(b), 8, rp, 1, 16, None, None) == -4  # align
     assert np.asarray(reqs).size == 1
+
+
+def test_unit_hash_headers_match_the_includes():
+    """A unit's hash (rpkt_gpu_build_info: parse=… tx=… walks=… fields=…, which ties the
+    committed profiles to kernel sources) covers exactly the csrc headers it includes,
+    directly or through another header."""
+    import re
+    from rpkt_amd import build
+    csrc = os.path.join(os.path.dirname(build.__file__), "csrc")
+
+    def includes(name, seen):
+        with open(os.path.join(csrc, name)) as fh:
+            for h in re.findall(r'#include "([^"/]+)"', fh.read()):
+                if h not in seen:
+                    seen.add(h)
+                    includes(h, seen)
+        return seen
+
+    for src in build.GPU_SRC:
+        u = os.path.basename(src)
+        assert set(build.UNIT_HEADERS[u]) == includes(u, set()), u
+    assert set(build.UNIT_HEADERS) == {os.path.basename(f) for f in build.GPU_SRC}
