@@ -82,7 +82,7 @@ def build_gpu(force=False, extra=()):
     the development library (-DRPKT_ABLATE)."""
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OUT, exist_ok=True)
-    deps = GPU_SRC + GPU_DEPS + HDR
+    deps = GPU_SRC + GPU_DEPS + HDR + [os.path.abspath(__file__)]   # the flags and hashes too
     if not (force or _stale(GPU_LIB, deps) or _stale(ABLATE_LIB, deps)):
         return GPU_LIB
     flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
