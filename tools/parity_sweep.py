@@ -8,8 +8,8 @@ difference and names the seed and entry point (a JSON line per seed, progress on
 
 Per seed: (a) a random packed or strided layout over the captures, configs 2/3/5/6 and
 the dual-stack fuzz (config 12) frames: the parse with a random flag set (with or without
-RPKT_F_IPV6) and flow events, compact records, both option-walk entry points over full and
-compact records, the layer walk; (b) a generator batch of a random config and size: the
+RPKT_F_IPV6) and flow events, compact records, a two-slot receive ring (80-B and compact),
+both option-walk entry points over full and compact records, the layer walk; (b) a generator batch of a random config and size: the
 build with random checksum flags over its (IPv4 and IPv6) records, the forward with and
 without RPKT_F_IPV6; (c) a fuzzed mbuf-chain batch (configs 8 / 12) through the chain
 parse.  Build and forward rewrite frames in place, so they run on generator batches
@@ -75,6 +75,21 @@ def check_layout(hb, rng):
         assert as_opts(oo.cpu().numpy()).tobytes() == want, "fused options (compact=%s)" % compact
         so = engine.options_batch(db, rr, compact=compact)
         assert as_opts(so.cpu().numpy()).tobytes() == want, "options (compact=%s)" % compact
+    # a receive ring: this layout and a strided generator batch as the slots of one launch
+    import torch
+    hb2 = gen.make_batch(int(rng.choice([2, 10, 12])), int(rng.integers(1, 3000)),
+                         seed=int(rng.integers(1, 1 << 30)))
+    dbs = [db, engine.DeviceBatch.from_host(hb2)]
+    rr = [engine.alloc_records(h.n) for h in (hb, hb2)]
+    evs = [torch.zeros(h.n, dtype=torch.int64, device="cuda") for h in (hb, hb2)]
+    engine.parse_ring(engine.ring_slots(dbs, rr, evs), flags | F_FLOW_EV, nb)
+    r16 = [torch.empty(h.n * 16, dtype=torch.uint8, device="cuda") for h in (hb, hb2)]
+    engine.parse_ring(engine.ring_slots(dbs, r16), flags, 0, compact=True)
+    for k, h in enumerate((hb, hb2)):
+        ok_, okev = (o, oev) if k == 0 else orecs(h, flags, nb, flow=True)
+        assert_same(as_records(rr[k].cpu().numpy()), ok_)
+        assert np.array_equal(evs[k].cpu().numpy().view(np.uint64), okev), "ring flow events"
+        assert_same16(as_records16(r16[k].cpu().numpy()), project16(ok_, flags))
     gl = engine.layers_batch(db).cpu().numpy().view(LAYERS_DTYPE)
     ol = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets, stride=hb.stride,
                              frame_len=hb.frame_len)
