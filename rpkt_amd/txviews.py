@@ -65,8 +65,12 @@ class CursorMut:
         self.extra = []              # (offset, bytes) the caller places in the frame
 
     def advance(self, n):
-        assert self.start + n <= self.frame_len
+        """cursors.rs CursorMut::advance: assert!(cnt <= self.remaining())."""
+        assert 0 <= n <= self.frame_len - self.start, "advance past the end"
         self.start += n
+
+    def cursor(self):
+        return self.start
 
     def chunk_headroom(self):
         return self.start
@@ -74,10 +78,16 @@ class CursorMut:
     def remaining(self):
         return self.frame_len - self.start
 
+    def trim_off(self, n):
+        """cursors.rs CursorMut::trim_off: the last n bytes leave the chunk
+        (assert!(cnt <= self.remaining()))."""
+        assert 0 <= n <= self.frame_len - self.start, "trim_off past the cursor"
+        self.frame_len -= n
+
     def move_back(self, n, data=None):
         """PktBufMut::move_back: n bytes of headroom become part of the packet (an
         extension header the caller writes: `data`, if given, is placed there)."""
-        assert n <= self.start
+        assert 0 <= n <= self.start, "move_back past the start"
         self.start -= n
         if data is not None:
             assert len(data) == n

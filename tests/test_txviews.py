@@ -278,3 +278,27 @@ def _headroom(n):
     c = tv.CursorMut(n + 10)
     c.advance(n)
     return c
+
+
+def test_cursor_mut_positions_and_panics():
+    """cursors.rs:321-412 (test_cursor_mut and the *_too_much should_panic tests) on the
+    host mirror: cursor / remaining after advance, move_back and trim_off over a 1000-B
+    buffer, and an AssertionError where rpkt panics."""
+    for c_pos in range(0, 1001, 37):
+        c = tv.CursorMut(1000)
+        c.advance(c_pos)
+        assert c.cursor() == c_pos and c.remaining() == 1000 - c_pos
+        c = tv.CursorMut(1000)
+        c.advance(1000)
+        c.move_back(c_pos)
+        assert c.cursor() == 1000 - c_pos and c.remaining() == c_pos
+    for c_pos in range(0, 701, 29):
+        c = tv.CursorMut(1000)
+        c.advance(300)
+        c.trim_off(c_pos)
+        assert c.remaining() == 1000 - 300 - c_pos
+    for op in ("advance", "move_back", "trim_off"):
+        c = tv.CursorMut(1000)
+        c.advance(407)
+        with pytest.raises(AssertionError):
+            getattr(c, op)(10000)
