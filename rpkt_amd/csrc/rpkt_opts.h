@@ -244,12 +244,186 @@ __device__ __forceinline__ Ip6Opts ip6_walk(const OptDw& dw, uint32_t l3, uint32
                    nhdr | (first << 8), gd, (uint32_t)trace, (uint32_t)(trace >> 32), end};
 }
 
+// One HopByHop / DestOptions header's option walk (the inner loop of ip6_walk) from a
+// fresh count: what the frame's walk adds for this header.
+struct Ip6Hdr {
+    uint32_t cnt, kinds, end, ra, g, gd;        // g: type_ | data length << 8 of a Generic
+    uint64_t trace;
+    bool mal, has_ra, has_g;
+};
+__device__ __forceinline__ Ip6Hdr ip6_hdr_walk(const OptDw& dw, uint32_t c, uint32_t hl) {
+    Ip6Hdr R{0u, 0u, 0u, 0u, 0u, 0u, 0ull, false, false, false};
+    const uint32_t s0 = c + 2u, nb = hl - 2u;
+    uint32_t pos = 0;
+    while (pos < nb) {
+        const uint32_t d = dw(s0 + pos);
+        const uint32_t t = d & 0xffu, rem = nb - pos;
+        if (t == 0u) {                                  // a run of Pad0 (up to 4 bytes)
+            uint32_t kz = d ? (uint32_t)__builtin_ctz(d) >> 3 : 4u;
+            kz = kz < rem ? kz : rem;
+            R.kinds |= 1u;
+            R.trace |= R.cnt < 16u ? (uint64_t)(0x1111u & ((1u << (4u * kz)) - 1u)) << (4u * R.cnt)
+                                   : 0ull;
+            R.cnt += kz;
+            pos += kz;
+            continue;
+        }
+        const uint32_t ln = ((d >> 8) & 0xffu) + 2u;                     // header_len
+        const bool ok = t == 5u ? (rem >= 4u && ln == 4u) : (rem >= 2u && ln <= rem);
+        if (!ok) {
+            R.mal = true;
+            break;
+        }
+        const uint32_t kind = t == 1u ? 1u : (t == 5u ? 2u : 3u);
+        if (kind == 2u) {                                                // router_alert
+            R.ra = be16_hi(d);
+            R.has_ra = true;
+        }
+        if (kind == 3u) {                               // Generic: type_, data length, the
+            const uint32_t gl = ln - 2u;                // slice's first bytes
+            const uint32_t v = bswap32(dw(s0 + pos + 2u));
+            R.g = t | (gl << 8);
+            R.gd = gl >= 4u ? v : v & ~(0xffffffffu >> (8u * gl));
+            R.has_g = true;
+        }
+        R.kinds |= 1u << kind;
+        R.trace |= R.cnt < 16u ? (uint64_t)(kind + 1u) << (4u * R.cnt) : 0ull;
+        R.cnt += 1u;
+        pos += ln;
+    }
+    R.end = pos;
+    return R;
+}
+
 // The IPv6 walks of the wave's IPv6 frames, while their windows are still in LDS (before
 // the rows are staged over them); a frame's bytes outside the window come from memory.
+// RPKT_IP6_DIST: a frame's walk is a chain of headers, each HopByHop / DestOptions one an
+// option walk of its own, and a wave used to step those option walks frame by frame:
+// header k of every frame, as many iterations as the frame with the most options in it
+// (config 11: 16.3 iterations per wave, by a count over its frames).  Here each lane first
+// walks its frame's header chain alone (one read per header), the wave's option headers
+// (19 per wave on config 11) are dealt out one per lane, walked at once (as many
+// iterations as the longest one: 5.8), and each frame folds its headers' results in chain
+// order -- counts and trace offsets add up, the last RouterAlert / Generic wins, the first
+// malformed header ends the walk.  A frame with more than kIp6Dist option headers walks
+// them itself, as before.
+#ifndef RPKT_IP6_DIST
+#define RPKT_IP6_DIST 1
+#endif
+constexpr uint32_t kIp6Dist = 3;
 __device__ __forceinline__ Ip6Opts ip6_walks(const OptSlices& S, const OptDw& dw) {
     Ip6Opts v{0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#if !RPKT_IP6_DIST
     if (__ballot(S.ip6) != 0 && S.ip6) v = ip6_walk(dw, S.l3, S.l4, S.nh0);
     return v;
+#else
+    // frames without extension headers have nothing to walk: their words are zero
+    const bool w = S.ip6 && S.l4 > S.l3 + 40u;
+    if (__ballot(w) == 0) return v;
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    // the frame's header chain: where its first kIp6Dist option headers start, and their
+    // lengths (the same loop as ip6_walk's, without the option steps)
+    uint32_t hc0 = 0, hc1 = 0, hc2 = 0, hh0 = 0, hh1 = 0, hh2 = 0, nopt = 0, first = 0;
+    if (w) {
+        uint32_t nh = S.nh0 < 256u ? S.nh0 : (dw(S.l3 + 4u) >> 16) & 0xffu;
+        uint32_t c = S.l3 + 40u;
+        for (int k = 0; k < RPKT_MAX_IP6_EXT && c < S.l4; ++k) {
+            const uint32_t d0 = dw(c);
+            const uint32_t b1 = (d0 >> 8) & 0xffu;
+            const uint32_t hl = nh == 44u ? 8u : (nh == 51u ? b1 * 4u + 8u : b1 * 8u + 8u);
+            if (nh == 0u || nh == 60u) {
+                hc0 = nopt == 0u ? c : hc0;
+                hh0 = nopt == 0u ? hl : hh0;
+                hc1 = nopt == 1u ? c : hc1;
+                hh1 = nopt == 1u ? hl : hh1;
+                hc2 = nopt == 2u ? c : hc2;
+                hh2 = nopt == 2u ? hl : hh2;
+                first = nopt == 0u ? nh : first;
+                nopt += 1u;
+            }
+            nh = d0 & 0xffu;
+            c += hl;
+        }
+    }
+    const bool serial = w && nopt > kIp6Dist;
+    const uint32_t m = w && !serial ? nopt : 0u;
+    // entries: frame l's option headers are P_l .. P_l + m_l - 1 (an exclusive scan of m)
+    uint32_t inc = m;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, kWave);
+        inc += lane >= (uint32_t)d ? y : 0u;
+    }
+    const uint32_t P = inc - m;
+    const uint32_t total = (uint32_t)__shfl((int)inc, kWave - 1, kWave);
+    const uint64_t slot = (uint64_t)(uintptr_t)dw.slot;
+    uint32_t cnt = 0, kinds = 0, stop = RPKT_OPT_NONE, end = 0, ra = 0, g = 0, gd = 0, nhdr = 0;
+    uint64_t trace = 0;
+    bool stopped = false;
+    for (uint32_t r0 = 0; r0 < total; r0 += (uint32_t)kWave) {          // wave-uniform
+        // entry E = r0 + lane: its frame is the last lane l with P_l <= E
+        const uint32_t E = r0 + lane;
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t st = kWave / 2; st >= 1u; st >>= 1) {
+            const uint32_t p = (uint32_t)__shfl((int)P, (int)(l + st), kWave);
+            l = p <= E ? l + st : l;
+        }
+        const uint32_t j = E - (uint32_t)__shfl((int)P, (int)l, kWave);
+        const uint32_t c0 = (uint32_t)__shfl((int)hc0, (int)l, kWave);
+        const uint32_t c1 = (uint32_t)__shfl((int)hc1, (int)l, kWave);
+        const uint32_t c2 = (uint32_t)__shfl((int)hc2, (int)l, kWave);
+        const uint32_t h0 = (uint32_t)__shfl((int)hh0, (int)l, kWave);
+        const uint32_t h1 = (uint32_t)__shfl((int)hh1, (int)l, kWave);
+        const uint32_t h2 = (uint32_t)__shfl((int)hh2, (int)l, kWave);
+        OptDw de = dw;                                  // frame l's window and offset
+        de.slot = reinterpret_cast<const uint8_t*>(
+            (uintptr_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)(slot >> 32), (int)l, kWave) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)slot, (int)l, kWave)));
+        de.bias = (uint32_t)__shfl((int)dw.bias, (int)l, kWave);
+        de.lo = (uint32_t)__shfl((int)dw.lo, (int)l, kWave);
+        de.hi = (uint32_t)__shfl((int)dw.hi, (int)l, kWave);
+        de.fo = (uint32_t)__shfl((int)dw.fo, (int)l, kWave);
+        Ip6Hdr R{0u, 0u, 0u, 0u, 0u, 0u, 0ull, false, false, false};
+        if (E < total)
+            R = ip6_hdr_walk(de, j == 0u ? c0 : (j == 1u ? c1 : c2), j == 0u ? h0 : (j == 1u ? h1 : h2));
+        // each frame folds its entries of this round, in chain order
+        const uint32_t flags = (R.mal ? 1u : 0u) | (R.has_ra ? 2u : 0u) | (R.has_g ? 4u : 0u);
+#pragma unroll
+        for (uint32_t jj = 0; jj < kIp6Dist; ++jj) {
+            const uint32_t Eo = P + jj;
+            const bool mine = jj < m && Eo >= r0 && Eo < r0 + (uint32_t)kWave;
+            const int src = (int)((Eo - r0) & (uint32_t)(kWave - 1));
+            const uint32_t rc = (uint32_t)__shfl((int)R.cnt, src, kWave);
+            const uint32_t rk = (uint32_t)__shfl((int)R.kinds, src, kWave);
+            const uint32_t re = (uint32_t)__shfl((int)R.end, src, kWave);
+            const uint32_t rr = (uint32_t)__shfl((int)R.ra, src, kWave);
+            const uint32_t rg = (uint32_t)__shfl((int)R.g, src, kWave);
+            const uint32_t rd = (uint32_t)__shfl((int)R.gd, src, kWave);
+            const uint32_t rf = (uint32_t)__shfl((int)flags, src, kWave);
+            const uint32_t tl = (uint32_t)__shfl((int)(uint32_t)R.trace, src, kWave);
+            const uint32_t th = (uint32_t)__shfl((int)(uint32_t)(R.trace >> 32), src, kWave);
+            if (mine && !stopped) {
+                const uint64_t rt = ((uint64_t)th << 32) | tl;
+                trace |= cnt < 16u ? rt << (4u * cnt) : 0ull;
+                cnt += rc;
+                kinds |= rk;
+                ra = (rf & 2u) ? rr : ra;
+                g = (rf & 4u) ? rg : g;
+                gd = (rf & 4u) ? rd : gd;
+                end = re;
+                nhdr += 1u;
+                stopped = (rf & 1u) != 0u;
+                stop = stopped ? (uint32_t)RPKT_OPT_MALFORMED : (uint32_t)RPKT_OPT_END;
+            }
+        }
+    }
+    if (w && !serial)
+        v = Ip6Opts{(cnt & 0xffu) | (stop << 8) | (kinds << 16), ra | ((g & 0xffu) << 16) | ((g >> 8) << 24),
+                    nhdr | (first << 8), gd, (uint32_t)trace, (uint32_t)(trace >> 32), end};
+    if (__ballot(serial) != 0 && serial) v = ip6_walk(dw, S.l3, S.l4, S.nh0);
+    return v;
+#endif
 }
 
 // The two walks (Ipv4OptionsIter::next, ipv4/generated.rs:1640-1722;
