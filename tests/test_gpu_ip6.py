@@ -214,3 +214,34 @@ def test_ip6_option_walks_fixtures_and_long_chains(torch, lead):
                                      opts=True))
     hb = host_batch(frames, lead)
     _opts_check(engine.DeviceBatch.from_host(hb), hb, F6)
+
+
+@pytest.mark.parametrize("lead", [0, 3])
+def test_ip6_option_headers_dealt_out(torch, lead):
+    """The distributed IPv6 option walk (rpkt_opts.h ip6_walks, RPKT_IP6_DIST): waves whose
+    every frame has three option headers (192 headers: three rounds of 64), frames with
+    four to eight (walked serially by their own lane), option headers around Routing /
+    Fragment / AH ones, malformed options mid-chain (the walk ends there), and frames with
+    none, mixed at random over several waves."""
+    rng = np.random.default_rng(505 + lead)
+    frames = []
+    for w in range(6):
+        for _ in range(64):
+            if w < 2:                                            # full waves of 3 headers
+                exts = [(0, 8 * int(rng.integers(1, 4))), (60, 8 * int(rng.integers(1, 3))),
+                        (60, 8 * int(rng.integers(1, 4)))]
+            else:
+                exts = []
+                for _ in range(int(rng.integers(0, 9))):
+                    t = int(rng.choice([0, 60, 60, 43, 44, 51]))
+                    hl = {0: 8 * int(rng.integers(1, 5)), 60: 8 * int(rng.integers(1, 5)),
+                          43: 24, 44: 8, 51: 12 + 4 * int(rng.integers(0, 3))}[t]
+                    exts.append((t, hl))
+                exts = exts[:8]
+            pl = rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes()
+            frames.append(_ip6_frame(rng, exts, int(rng.choice([6, 17])), pl, opts=True))
+    hb = host_batch(frames, lead)
+    want, o = _opts_check(engine.DeviceBatch.from_host(hb), hb, F6)
+    n_hdrs = ip6_opts_view(want)["n_hdrs"]
+    assert (n_hdrs[lead > 0:][:128] == 3).mean() > 0.5 and (n_hdrs > 3).any()
+    assert (want["ip_stop"][is_ip6(o)] == 3).any()               # malformed walks
