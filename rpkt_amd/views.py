@@ -117,6 +117,22 @@ class Cursor:
     def remaining(self):
         return self.length
 
+    # The raw moves of cursors.rs Cursor (:63-99), in place as rpkt's `&mut self`
+    # methods: the position leaves the parsed chain (a header view parses only where the
+    # record placed one), so a moved cursor's stage is "raw".  rpkt panics past the
+    # bounds; here an AssertionError.
+    def advance(self, n):
+        assert 0 <= n <= self.length, "advance past the end"
+        self.stage, self.off, self.length = "raw", self.off + n, self.length - n
+
+    def move_back(self, n):
+        assert 0 <= n <= self.off, "move_back past the start"
+        self.stage, self.off, self.length = "raw", self.off - n, self.length + n
+
+    def trim_off(self, n):
+        assert 0 <= n <= self.length, "trim_off past the cursor"
+        self.stage, self.length = "raw", self.length - n
+
     def chunk(self):
         if self.frame is None:
             raise ValueError("frame bytes were not supplied to Packet()")

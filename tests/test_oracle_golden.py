@@ -254,3 +254,36 @@ def test_packet_l4_loop_over_config1():
     bad[3] ^= 0x100
     assert oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, hb.frame_len or hb.stride, 2,
                                  tuple(bad)) == 2 * hb.n
+
+
+def test_cursor_positions_and_panics():
+    """cursors.rs:288-320 (test_cursor) and its *_too_much should_panic tests on the host
+    view's Cursor over a 1000-B frame: cursor / remaining / chunk after advance, move_back
+    and trim_off; an AssertionError where rpkt panics."""
+    from rpkt_amd import views
+    from rpkt_amd.records import REC_DTYPE
+    rec = np.zeros(1, dtype=REC_DTYPE)[0]
+    rec["frame_len"] = 1000
+    b = bytes([10]) * 1000
+    for c_pos in range(0, 1001, 41):
+        c = views.Packet(rec, b)
+        c.advance(c_pos)
+        assert c.cursor() == c_pos and c.remaining() == 1000 - c_pos and c.chunk() == b[c_pos:]
+        c = views.Packet(rec, b)
+        c.advance(1000)
+        c.move_back(c_pos)
+        assert c.cursor() == 1000 - c_pos and c.remaining() == c_pos
+        assert c.chunk() == b[1000 - c_pos:]
+    for c_pos in range(0, 701, 23):
+        c = views.Packet(rec, b)
+        c.advance(300)
+        c.trim_off(c_pos)
+        assert c.remaining() == 700 - c_pos and c.chunk() == b[300:1000 - c_pos]
+    for op in ("advance", "move_back", "trim_off"):
+        c = views.Packet(rec, b)
+        c.advance(407)
+        with pytest.raises(AssertionError):
+            getattr(c, op)(10000)
+    c = views.Packet(rec, b)
+    c.advance(0)
+    assert not views.EtherFrame.parse(c).is_ok()          # a moved cursor is no parse start
