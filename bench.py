@@ -388,7 +388,9 @@ def flatten_all_cores(out):
     value (records that keep only the top level of cpu_baseline still carry it)."""
     a = out["all_cores"]
     out.update(all_cores_mpps=a["value"], all_cores_gb_per_s=a["gb_per_s"],
-               all_cores_threads=a["cores"])
+               all_cores_threads=a["cores"],
+               # all-threads rate over the 1-thread rate: how far the static partition scales
+               all_cores_scaling=round(a["value"] / out["value"], 2) if out["value"] else None)
     return out
 
 
@@ -405,9 +407,13 @@ def cpu_baseline_chains(hc, gpu_recs, flags, seconds, threads_all, max_bytes=256
     nbytes = int(hc.lens()[:m].sum())
     sample = "first %d chains (%.0f MB, %d segments) of the batch" % (m, nbytes / 1e6,
                                                                        segs.shape[0])
-    reps, dt = timed_reps(lambda: oracle.parse_chains(hc.buf, segs, first, flags), seconds)
+    # the record buffer is allocated once, outside the timed reps (the reference's harness
+    # allocates nothing per iteration, benches/rpkt/rpkt_parse.rs:108-140); timed_reps'
+    # untimed first call first-touches each thread's slice of it
+    out = np.empty_like(o)
+    reps, dt = timed_reps(lambda: oracle.parse_chains(hc.buf, segs, first, flags, out=out), seconds)
     reps_a, dt_a = timed_reps(lambda: oracle.parse_chains(hc.buf, segs, first, flags,
-                                                          threads=threads_all), seconds)
+                                                          threads=threads_all, out=out), seconds)
     out = cpu_fields(m * reps / dt / 1e6, nbytes * reps / dt / 1e9, 1,
                      "%d reps x %s, 1 thread" % (reps, sample), reps, dt, build)
     out.update(kind="port", cpu_model=cpu_model(), host_logical_cpus=os.cpu_count(),
@@ -416,6 +422,24 @@ def cpu_baseline_chains(hc, gpu_recs, flags, seconds, threads_all, max_bytes=256
                                     % (reps_a, sample, threads_all), reps_a, dt_a, build),
                gpu_parity_on_sample=bool(gpu_recs[:m].tobytes() == o.tobytes()))
     return flatten_all_cores(out)
+
+
+def cpu_parse_callable(oracle, hb, flags, threads):
+    """The timed body of the CPU baseline: the oracle's parse of the sample into a record
+    buffer allocated here, once (the reference's criterion loop allocates nothing per
+    iteration, benches/rpkt/rpkt_parse.rs:108-140).  timed_reps' untimed first call
+    first-touches each thread's slice of it, so the timed calls measure the parse alone
+    (tests/test_bench_cli.py checks that a call allocates nothing)."""
+    from rpkt_amd.records import REC_DTYPE
+    out = np.empty(hb.n, dtype=REC_DTYPE)
+    frames = np.ascontiguousarray(hb.frames, dtype=np.uint8)
+    offs = None if hb.offsets is None else np.ascontiguousarray(hb.offsets, dtype=np.uint32)
+
+    def run():
+        oracle.parse_batch(frames, hb.n, flags=flags, offsets=offs, stride=hb.stride,
+                           frame_len=hb.frame_len, threads=threads, out=out)
+    run.out = out
+    return run
 
 
 def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
@@ -428,13 +452,11 @@ def cpu_baseline(hb, gpu_recs, flags, seconds, threads_all):
     n = hb.n
     nbytes = int(hb.lens().sum())
 
-    def run(threads):
-        return oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets,
-                                  stride=hb.stride, frame_len=hb.frame_len, threads=threads)
-    o = run(1)
+    o = oracle.parse_batch(hb.frames, n, flags=flags, offsets=hb.offsets, stride=hb.stride,
+                           frame_len=hb.frame_len)
     sample = "first %d frames (%.0f MB) of the batch" % (n, nbytes / 1e6)
-    reps, dt = timed_reps(lambda: run(1), seconds)
-    reps_a, dt_a = timed_reps(lambda: run(threads_all), seconds)
+    reps, dt = timed_reps(cpu_parse_callable(oracle, hb, flags, 1), seconds)
+    reps_a, dt_a = timed_reps(cpu_parse_callable(oracle, hb, flags, threads_all), seconds)
     out = cpu_fields(n * reps / dt / 1e6, nbytes * reps / dt / 1e9, 1,
                      "%d reps x %s, 1 thread" % (reps, sample), reps, dt, build)
     out.update(kind="port", cpu_model=cpu_model(), host_logical_cpus=os.cpu_count(),
@@ -467,8 +489,19 @@ def run_config1(args):
     bad += oracle.packet_l4_loop(hb.frames, hb.n, hb.stride, flen, reps, want)
     dt = time.perf_counter() - t0
     ns = dt / (reps * hb.n) * 1e9
+    # the same loop on every usable host thread at once: each thread
+    # makes reps_a passes over the 1,000 frames
+    threads = max(1, args.cpu_threads or usable_cpus())
+    reps_a = max(1, reps // 2)
+    t0 = time.perf_counter()
+    bad += oracle.packet_l4_loop_mt(hb.frames, hb.n, hb.stride, flen, reps_a, want, threads)
+    dt_a = time.perf_counter() - t0
+    mpps_a = threads * reps_a * hb.n / dt_a / 1e6
     return {"ns_per_pkt": round(ns, 3), "mpps": round(1e3 / ns, 2), "cores": 1,
             "frames": hb.n, "frame_bytes": 64, "reps": reps, "seconds": round(dt, 2),
+            "all_cores_mpps": round(mpps_a, 2), "all_cores_threads": threads,
+            "all_cores_seconds": round(dt_a, 2),
+            "all_cores_scaling": round(mpps_a / (1e3 / ns), 2),
             "asserts_failed": bad, "kind": "port", "build": build, "cpu_model": cpu_model(),
             "what": "benches/rpkt packet_l4 (rpkt_parse.rs:62-80) restated in C, per frame"}
 
@@ -540,6 +573,9 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
     mpps = frames_job * args.steps / wall / 1e6
     gbps = bytes_job * args.steps / wall / 1e9
     achieved = alg_step / (kern_ms / 1e3) / 1e9
+    # N > 1: every rank's achieved GB/s summed (each rank has its own HBM), beside the
+    # per-rank fraction `frac` (a collective: every rank calls it)
+    achieved_all = sum_over_ranks(achieved, world) if world > 1 else None
     traffic, tsrc = pmc_traffic(cfg, compact, opts, hbs[0].n)
     out = {
         "mpps": mpps, "frame_gb_per_s": gbps, "ms_per_step": wall / args.steps * 1e3,
@@ -553,6 +589,9 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         "flags": FLAG_NAMES[flags], "layout": layout_name(hbs[0]),
         "record_bytes": rec_bytes,
     }
+    if achieved_all is not None:
+        out["roofline"].update(achieved_all_ranks=round(achieved_all, 1),
+                               peak_all_ranks=HBM_PEAK_GBS * world)
     if compact:
         out["what"] = ("rpkt_gpu_parse_batch_compact: the same parse + sums, 16-B records "
                        "(status, offsets, sums, verdicts)")
@@ -573,14 +612,31 @@ def run_config(cfg, args, rank, world, cpu=False, compact=False, opts=False, str
         rdist.reduce_counters(zeros, n_buckets=nb, via=args.reduce_comm)
         torch.cuda.synchronize()
         barrier(world)
-        t0 = time.perf_counter()
+        # the reduce time: REDUCE_SAMPLES reduces of a scratch copy (each one sums in place,
+        # so the real counters are reduced once, below), each bracketed by a barrier and a
+        # synchronize, the max over ranks per sample; median, min and max reported (one
+        # latency-bound 262-KB all-reduce is too short for a single sample to mean much)
+        scratch = flow["counters"].clone()
+        samples = []
+        for _ in range(REDUCE_SAMPLES):
+            torch.cuda.synchronize()
+            barrier(world)
+            t0 = time.perf_counter()
+            rdist.reduce_counters(scratch, n_buckets=nb, via=args.reduce_comm)
+            torch.cuda.synchronize()
+            samples.append(max_over_ranks(time.perf_counter() - t0, world) * 1e3)
+        del scratch
+        torch.cuda.synchronize()
+        barrier(world)
         # rpkt_gpu_flow_reduce (RCCL, C ABI) when every rank can call it, else torch's
         # all-reduce on every rank; a failure after the group chose the C ABI raises
         rdist.reduce_counters(flow["counters"], n_buckets=nb, via=args.reduce_comm)
         torch.cuda.synchronize()
-        red = time.perf_counter() - t0
         c = rdist.counters_as_u64(flow["counters"])
-        out["flow_reduce_ms"] = max_over_ranks(red, world) * 1e3
+        out["flow_reduce_ms"] = float(np.median(samples))
+        out["flow_reduce_ms_min"] = min(samples)
+        out["flow_reduce_ms_max"] = max(samples)
+        out["flow_reduce_samples"] = len(samples)
         out["flow_reduce_via"] = rdist.last_reduce_path
         if rdist.last_reduce_error:
             out["flow_reduce_error"] = "C ABI reduce not taken: %s" % rdist.last_reduce_error
@@ -1020,9 +1076,12 @@ def run_tx(cfg, mode, args, rank, world):
 
 LINE_MAX = 8000           # the driver keeps an 8,000-char tail of stdout: the line fits it
 CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "gb_per_s", "all_cores_mpps",
-            "all_cores_gb_per_s", "all_cores_threads", "gpu_parity_on_sample", "cpu_model")
-FLOW_KEYS = ("flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified", "flow_reduce_error",
-             "flow_pkts_total", "flow_pkts_expected")
+            "all_cores_gb_per_s", "all_cores_threads", "all_cores_scaling", "gpu_parity_on_sample",
+            "cpu_model")
+FLOW_KEYS = ("flow_reduce_ms", "flow_reduce_ms_min", "flow_reduce_ms_max", "flow_reduce_samples",
+             "flow_reduce_via", "flow_reduce_verified", "flow_reduce_error", "flow_pkts_total",
+             "flow_pkts_expected")
+REDUCE_SAMPLES = 20       # counter reduces timed per config-4 leg (median, min, max reported)
 
 
 def _r(x, nd=4):
@@ -1037,7 +1096,10 @@ def leg_summary(v):
         t, a = rf.get("traffic"), rf.get("alg_bytes_per_launch")
         s = {"kernel_ms": _r(v.get("kernel_ms"), 5), "ms_per_step": _r(v.get("ms_per_step"), 5),
              "frac": rf.get("frac"), "traffic_ratio": round(t / a, 4) if t and a else None}
-        for k in ("mpps", "flow_reduce_ms", "flow_reduce_via", "flow_reduce_verified"):
+        if "achieved_all_ranks" in rf:
+            s["achieved_all_ranks"] = rf["achieved_all_ranks"]
+        for k in ("mpps", "flow_reduce_ms", "flow_reduce_ms_min", "flow_reduce_ms_max",
+                  "flow_reduce_via", "flow_reduce_verified"):
             if k in v:
                 s[k] = _r(v[k], 3)
         return s

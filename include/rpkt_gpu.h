@@ -503,7 +503,11 @@ typedef struct rpkt_opts {
 
 /* Walk the IPv4 and TCP options of every frame of a parsed batch: recs_dev from
  * rpkt_gpu_parse_batch on the same batch locates the slices (ip: [l3 + 20, l4),
- * tcp: [l4 + 20, payload_off) for status OK / TCP).  opts_dev n * 64 B, 16-B aligned. */
+ * tcp: [l4 + 20, payload_off) for status OK / TCP).  opts_dev n * 64 B, 16-B aligned.
+ * For an IPv6 record the first header of the extension chain is the record's
+ * ip6_next_header (byte 30), which the parse copied from frame byte l3 + 6: the records
+ * must come from a parse of these same frames (the compact entry below, whose record has
+ * no such field, reads frame byte l3 + 6 itself; both agree whenever that holds). */
 int rpkt_gpu_options_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
                            rpkt_opts_t* opts_dev, void* stream);
 

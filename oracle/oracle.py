@@ -93,6 +93,9 @@ def lib():
                                             ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
                                             ctypes.c_uint16]
         L.oracle_packet_l4_loop.restype = ctypes.c_uint64
+        L.oracle_packet_l4_loop_mt.argtypes = (L.oracle_packet_l4_loop.argtypes[:5] + [ctypes.c_int]
+                                               + L.oracle_packet_l4_loop.argtypes[5:])
+        L.oracle_packet_l4_loop_mt.restype = ctypes.c_uint64
         L.oracle_parse_chains_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
@@ -165,14 +168,29 @@ def parse_one(frame, flags=3):
     return rec[0]
 
 
+def _out_buffer(out, n, dtype, what):
+    """A caller's preallocated result array (checked), or a fresh zeroed one."""
+    if out is None:
+        return np.zeros(n, dtype=dtype)
+    if out.dtype != dtype or out.shape != (n,) or not out.flags.c_contiguous:
+        raise ValueError("%s: expected a contiguous (%d,) %s array" % (what, n, dtype))
+    return out
+
+
 def parse_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0, n_buckets=0,
-                threads=1, flow_ev=False):
-    """Oracle records (and optionally flow events) for a host batch."""
+                threads=1, flow_ev=False, out=None, ev_out=None):
+    """Oracle records (and optionally flow events) for a host batch.  out / ev_out: arrays
+    the records / events are written into (every record is written whole, so a reused
+    buffer needs no zeroing): a timed loop then allocates nothing per call."""
     from rpkt_amd.records import REC_DTYPE
-    frames = np.ascontiguousarray(frames, dtype=np.uint8)
-    recs = np.zeros(n, dtype=REC_DTYPE)
-    ev = np.zeros(n, dtype=np.uint64) if flow_ev else None
-    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    frames = frames if (isinstance(frames, np.ndarray) and frames.dtype == np.uint8
+                        and frames.flags.c_contiguous) else np.ascontiguousarray(frames, dtype=np.uint8)
+    recs = _out_buffer(out, n, REC_DTYPE, "out")
+    ev = _out_buffer(ev_out, n, np.uint64, "ev_out") if (flow_ev or ev_out is not None) else None
+    flow_ev = ev is not None
+    offs = offsets if (offsets is None or (isinstance(offsets, np.ndarray) and offsets.dtype == np.uint32
+                                           and offsets.flags.c_contiguous)) \
+        else np.ascontiguousarray(offsets, dtype=np.uint32)
     if threads > 1:
         lib().oracle_parse_batch_mt(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
                                     flags, n_buckets, _ptr(recs), _ptr(ev), threads)
@@ -182,16 +200,19 @@ def parse_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0, n_bucke
     return (recs, ev) if flow_ev else recs
 
 
-def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False, threads=1):
+def parse_chains(buf, segs, chain_first, flags=3, n_buckets=0, flow_ev=False, threads=1,
+                 out=None, ev_out=None):
     """Oracle records for mbuf chains (rpkt_gpu_parse_chains arguments, host memory):
-    segs = u32 (offset, length) pairs into buf, chain_first = n_chains + 1 entries."""
+    segs = u32 (offset, length) pairs into buf, chain_first = n_chains + 1 entries.
+    out / ev_out: preallocated results, as parse_batch."""
     from rpkt_amd.records import REC_DTYPE
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     segs = np.ascontiguousarray(segs, dtype=np.uint32).reshape(-1)
     cf = np.ascontiguousarray(chain_first, dtype=np.uint32)
     n = cf.size - 1
-    recs = np.zeros(n, dtype=REC_DTYPE)
-    ev = np.zeros(n, dtype=np.uint64) if flow_ev else None
+    recs = _out_buffer(out, n, REC_DTYPE, "out")
+    ev = _out_buffer(ev_out, n, np.uint64, "ev_out") if (flow_ev or ev_out is not None) else None
+    flow_ev = ev is not None
     if threads > 1:
         lib().oracle_parse_chains_mt(_ptr(buf), buf.size, _ptr(segs), segs.size // 2, _ptr(cf), n,
                                      flags, n_buckets, _ptr(recs), _ptr(ev), threads)
@@ -214,6 +235,14 @@ def packet_l4_loop(frames, n, stride, frame_len, reps, want):
     C); returns the number of failed frames over all passes."""
     f = np.ascontiguousarray(frames, dtype=np.uint8)
     return int(lib().oracle_packet_l4_loop(_ptr(f), n, stride, frame_len, reps, *want))
+
+
+def packet_l4_loop_mt(frames, n, stride, frame_len, reps, want, threads):
+    """packet_l4_loop on `threads` host threads at once, each making `reps` passes over
+    the same n frames (criterion's loop run once per core); returns the failed frames
+    over all threads and passes."""
+    f = np.ascontiguousarray(frames, dtype=np.uint8)
+    return int(lib().oracle_packet_l4_loop_mt(_ptr(f), n, stride, frame_len, reps, threads, *want))
 
 
 def pbuf_script(seg_lens, ops):

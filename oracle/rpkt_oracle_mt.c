@@ -96,3 +96,48 @@ int oracle_parse_chains_mt(const uint8_t* buf, uint64_t buf_bytes, const uint32_
     free(jobs);
     return 0;
 }
+
+/* Config 1's loop on every usable host thread (the all-cores figure beside the 1-thread
+ * one): each thread makes `reps` passes of packet_l4 over the same
+ * n frames, as criterion's b.iter would run once per core
+ * (benches/rpkt/rpkt_parse.rs:108-140); returns the failed frames summed over threads. */
+uint64_t oracle_packet_l4_loop(const uint8_t* frames, uint32_t n, uint32_t stride, uint32_t len,
+                               uint32_t reps, uint32_t want_src, uint32_t want_dst,
+                               uint16_t want_ip_ck, uint16_t want_ident, uint16_t want_sport,
+                               uint16_t want_dport, uint16_t want_ulen, uint16_t want_udp_ck);
+
+typedef struct {
+    const uint8_t* frames; uint32_t n, stride, len, reps, src, dst;
+    uint16_t ip_ck, ident, sport, dport, ulen, udp_ck; uint64_t bad;
+} l4_job_t;
+
+static void* run_l4(void* p) {
+    l4_job_t* j = (l4_job_t*)p;
+    j->bad = oracle_packet_l4_loop(j->frames, j->n, j->stride, j->len, j->reps, j->src, j->dst,
+                                   j->ip_ck, j->ident, j->sport, j->dport, j->ulen, j->udp_ck);
+    return NULL;
+}
+
+uint64_t oracle_packet_l4_loop_mt(const uint8_t* frames, uint32_t n, uint32_t stride, uint32_t len,
+                                  uint32_t reps, int nthreads, uint32_t want_src, uint32_t want_dst,
+                                  uint16_t want_ip_ck, uint16_t want_ident, uint16_t want_sport,
+                                  uint16_t want_dport, uint16_t want_ulen, uint16_t want_udp_ck) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    l4_job_t* jobs = (l4_job_t*)calloc((size_t)nthreads, sizeof(l4_job_t));
+    if (!th || !jobs) { free(th); free(jobs); return ~0ull; }
+    for (int t = 0; t < nthreads; t++) {
+        l4_job_t j = {frames, n, stride, len, reps, want_src, want_dst, want_ip_ck, want_ident,
+                      want_sport, want_dport, want_ulen, want_udp_ck, 0};
+        jobs[t] = j;
+        pthread_create(&th[t], NULL, run_l4, &jobs[t]);
+    }
+    uint64_t bad = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        bad += jobs[t].bad;
+    }
+    free(th);
+    free(jobs);
+    return bad;
+}

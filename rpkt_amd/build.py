@@ -44,6 +44,9 @@ UNIT_HEADERS = {"rpkt_parse.hip": ("rpkt_common.h", "rpkt_opts.h"),
                 "rpkt_fields.hip": ("rpkt_common.h",),
                 "rpkt_abi.hip": ("rpkt_common.h",),
                 "rpkt_coll.hip": ("rpkt_common.h",)}
+# every unit has its header list (a unit added to GPU_SRC without one would make
+# source_hash raise at the first build: fail here, at import, instead)
+assert set(UNIT_HEADERS) == {os.path.basename(f) for f in GPU_SRC}, "UNIT_HEADERS vs GPU_SRC"
 GEN_SRC = [os.path.join(HERE, "csrc", "rpkt_gen.cpp")]
 HDR = [os.path.join(ROOT, "include", "rpkt_gpu.h"), os.path.join(ROOT, "include", "rpkt_protocols.h")]
 
@@ -55,11 +58,14 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def source_hash(units=None):
-    """Short hash of the engine sources (or of some units plus the shared headers):
-    ties profiles/ numbers to a kernel build."""
+def source_hash(units=None, defines=()):
+    """Short hash of the engine sources (or of some units plus the shared headers) and of
+    the compile-time switches they are built with (`defines`, e.g. an ablation build's
+    -DRPKT_IP6_DIST=0): ties profiles/ numbers to a kernel build."""
     import hashlib
     h = hashlib.sha1()
+    if defines:
+        h.update(("\0".join(defines) + "\0").encode())
     srcs = GPU_SRC if units is None else [f for f in GPU_SRC if os.path.basename(f) in units]
     deps = GPU_DEPS
     if units is not None:                  # the headers those units include
@@ -70,10 +76,10 @@ def source_hash(units=None):
     return h.hexdigest()[:12]
 
 
-def unit_hashes():
-    """Per-unit hashes (unit file + shared headers), so a profile of one kernel family
-    stays valid while another unit changes: "parse=... tx=... walks=... fields=..."."""
-    return " ".join("%s=%s" % (u, source_hash(["rpkt_%s.hip" % u]))
+def unit_hashes(defines=()):
+    """Per-unit hashes (unit file + shared headers + compile switches), so a profile of one
+    kernel family stays valid while another unit changes: "parse=... tx=... walks=..."."""
+    return " ".join("%s=%s" % (u, source_hash(["rpkt_%s.hip" % u], defines))
                     for u in ("parse", "tx", "walks", "fields"))
 
 
@@ -85,9 +91,10 @@ def build_gpu(force=False, extra=()):
     deps = GPU_SRC + GPU_DEPS + HDR + [os.path.abspath(__file__)]   # the flags and hashes too
     if not (force or _stale(GPU_LIB, deps) or _stale(ABLATE_LIB, deps)):
         return GPU_LIB
+    defines = tuple(x for x in extra if x.startswith("-D"))
     flags = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-             '-DRPKT_SRC_HASH="%s"' % source_hash(), '-DRPKT_UNIT_HASHES="%s"' % unit_hashes()] + \
-        list(extra)
+             '-DRPKT_SRC_HASH="%s"' % source_hash(None, defines),
+             '-DRPKT_UNIT_HASHES="%s"' % unit_hashes(defines)] + list(extra)
     units = [(f, os.path.basename(f)[:-4], []) for f in GPU_SRC]
     units += [(os.path.join(HERE, "csrc", src), obj[:-2], d) for src, obj, d in SECOND_COMPILES]
     libs = {GPU_LIB: [], ABLATE_LIB: []}

@@ -633,6 +633,9 @@ int RPKT_TX_FN(rpkt_gpu_build_batch)(const rpkt_batch_t* b, const rpkt_rec_t* re
 int RPKT_TX_FN(rpkt_gpu_forward_batch)(const rpkt_batch_t* b, const rpkt_fwd_t* fwd,
                                        uint8_t* keep_dev, void* stream) {
     if (!b || !fwd || !keep_dev) return RPKT_E_INVAL;
+    // unknown bits (a caller that left the old `reserved` field uninitialised) are refused,
+    // as rpkt_gpu_build_batch refuses unknown build flags
+    if (fwd->flags & ~(uint32_t)RPKT_F_IPV6) return RPKT_E_INVAL;
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev || (fwd->n_forbid && !fwd->forbid_dev)) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;

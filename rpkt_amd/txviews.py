@@ -132,6 +132,12 @@ class CursorMut:
                 r["ip_checksum"] = _be16(b, 10)
                 r["ip_src"], r["ip_dst"] = _be32(b, 12), _be32(b, 16)
                 r["l4_off"] = l3 + v.header_len()
+                if b[9] in (6, 17) and not any(k in ("udp", "tcp") for k, _, _ in self.layers):
+                    # the record's ip_protocol is both the header byte and what the build
+                    # writes at l4_off (a UDP / TCP header): with no Udp / Tcp view the build
+                    # would overwrite the caller's bytes there, which prepend_header leaves
+                    raise ValueError("IPv4 protocol %d without a Udp/Tcp view: the build "
+                                     "writes that header; prepend it with its view" % b[9])
                 if v.header_len() > 20:
                     extra.append((off - base + 20, bytes(v.b[20:])))
             elif kind == "ipv6":
@@ -143,10 +149,15 @@ class CursorMut:
                 raw[30], raw[31] = b[6], b[7]
                 extra.append((off - base + 8, bytes(b[8:40])))
                 up = [x for x in self.layers if x[0] in ("udp", "tcp")]
-                l4 = (up[0][1] - base) if up else (v.end - base)
-                n_ext = len([x for x in self.layers if x[0] == "raw" and x[1] >= off])
-                raw[32] = n_ext
-                r["ip_protocol"] = up[0][2].proto if up else b[6]
+                raws = [(o, n) for k, o, n in self.layers if k == "raw" and o >= off]
+                # with no Udp / Tcp view the upper layer starts after the extension headers
+                # placed with move_back, and the record's upper-layer protocol (byte 33) is
+                # 59, No Next Header: the build writes no L4 header over the caller's bytes
+                # there (next_header, byte 30, stays the header's own)
+                l4 = (up[0][1] - base) if up else max([v.end - base] +
+                                                      [o + n - base for o, n in raws])
+                raw[32] = len(raws)
+                r["ip_protocol"] = up[0][2].proto if up else 59
                 pd = l3 + 24 if v.pdst is None else v.pdst
                 raw[34:36] = np.frombuffer(int(pd).to_bytes(2, "little"), np.uint8)
                 r["l4_off"] = l4

@@ -301,3 +301,21 @@ def test_unit_hash_headers_match_the_includes():
         u = os.path.basename(src)
         assert set(build.UNIT_HEADERS[u]) == includes(u, set()), u
     assert set(build.UNIT_HEADERS) == {os.path.basename(f) for f in build.GPU_SRC}
+
+
+def test_forward_refuses_unknown_flags_without_launch(L):
+    """rpkt_fwd_t.flags (was `reserved`): any bit but RPKT_F_IPV6 is refused before anything
+    is launched (a caller that left the old field uninitialised gets RPKT_E_INVAL, not
+    IPv6 forwarding), in the 128-B and the 64-B-window (strided short frames) entry."""
+    fwd = engine.Fwd()
+    keep = 4096
+    for stride in (64, 1500):                        # the w64 and the 128-B compile
+        d = engine.Batch(4096, stride * 10, None, stride, 0, 10, 0)
+        for bad in (1, 4, 16, 0x80000000, 8 | 2):
+            fwd.flags = bad
+            assert L.rpkt_gpu_forward_batch(ctypes.byref(d), ctypes.byref(fwd), keep, None) == -1
+    d = engine.Batch(None, 0, None, 64, 0, 0, 0)
+    fwd.flags = 8
+    assert L.rpkt_gpu_forward_batch(ctypes.byref(d), ctypes.byref(fwd), keep, None) == 0   # n == 0
+    fwd.flags = 16
+    assert L.rpkt_gpu_forward_batch(ctypes.byref(d), ctypes.byref(fwd), keep, None) == -1

@@ -129,3 +129,54 @@ def test_n_rank_default_leg_set():
     allg = bench.resolve_legs(ns(all_legs=True), 8)
     assert allg.tx == one.tx and allg.also == one.also
     assert bench.resolve_legs(ns(tx="layers9"), 8).tx == "layers9"
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_cpu_baseline_timed_call_allocates_nothing(threads):
+    """The CPU baseline's timed body (bench.cpu_parse_callable) writes into a record
+    buffer made once: after the untimed first call, a call allocates nothing the size of
+    the records (tracemalloc sees numpy's buffers), and the records equal the oracle's."""
+    import tracemalloc
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle import oracle
+    from rpkt_amd import gen
+    hb = gen.make_batch(2, 4096)
+    fn = bench.cpu_parse_callable(oracle, hb, gen.FLAGS[2], threads)
+    fn()                                               # the untimed first call (first touch)
+    rec_bytes = fn.out.nbytes
+    tracemalloc.start()
+    try:
+        base = tracemalloc.get_traced_memory()[0]
+        tracemalloc.reset_peak()
+        for _ in range(5):
+            fn()
+        cur, peak = tracemalloc.get_traced_memory()
+    finally:
+        tracemalloc.stop()
+    assert peak - base < rec_bytes // 20, (peak - base, rec_bytes)
+    assert abs(cur - base) < 4096, (cur, base)
+    want = oracle.parse_batch(hb.frames, hb.n, flags=gen.FLAGS[2], stride=hb.stride,
+                              frame_len=hb.frame_len)
+    assert fn.out.tobytes() == want.tobytes()
+
+
+def test_packet_l4_all_cores_agrees():
+    """Config 1's all-cores loop: every thread's passes find no failed assert, and it
+    counts failures like the 1-thread loop on a corrupted frame."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from oracle import oracle
+    from rpkt_amd import gen
+    hb = gen.make_batch(1)
+    r = oracle.parse_batch(hb.frames, hb.n, flags=3, stride=hb.stride)
+    keys = ("ip_src", "ip_dst", "ip_checksum", "ip_ident", "src_port", "dst_port",
+            "l4_word6", "l4_checksum")
+    want = tuple(int(r[k][0]) for k in keys)
+    flen = hb.frame_len or hb.stride
+    assert oracle.packet_l4_loop_mt(hb.frames, hb.n, hb.stride, flen, 3, want, 4) == 0
+    f = np.array(hb.frames, copy=True)
+    f[hb.stride * 7 + 40] ^= 0xff                      # frame 7: another source port
+    one = oracle.packet_l4_loop(f, hb.n, hb.stride, flen, 2, want)
+    assert one == 2
+    assert oracle.packet_l4_loop_mt(f, hb.n, hb.stride, flen, 2, want, 4) == 4 * one

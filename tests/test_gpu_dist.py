@@ -299,6 +299,13 @@ def test_bench_nccl_ranks_sharing_one_gpu(tmp_path, comm):
     assert line["flow_reduce_via"] == ("rccl_own" if comm == "own" else "rccl"), line
     assert line["flow_reduce_verified"] is True
     assert line["flow_pkts_total"] == line["flow_pkts_expected"] > 0
+    # the reduce as the median of 20 timed reduces (min <= median <= max), and the summed
+    # achieved GB/s of both ranks beside the per-rank fraction
+    assert line["flow_reduce_samples"] == 20
+    assert 0 < line["flow_reduce_ms_min"] <= line["flow_reduce_ms"] <= line["flow_reduce_ms_max"]
+    rf = line["roofline"]
+    assert rf["peak_all_ranks"] == 2 * rf["peak"] and rf["achieved_all_ranks"] > rf["achieved"]
+    assert len(json.dumps(line)) < 8000
 
 
 def test_bench_under_torchrun_as_the_driver_launches_it(tmp_path):

@@ -228,3 +228,25 @@ def test_build_from_host_build_views(torch):
     hb = gen.HostBatch(0, len(lens), 0, buf, offs, 0, 0)
     for flags in (0, 3):
         check_build(torch, hb, recs, flags)
+
+
+def test_build_ip6_rfc8200_fixture(torch):
+    """tests/golden/ip6_tx.json (checksums from RFC 8200 section 8.1 + RFC 1071 alone, see
+    tests/golden/make_ip6_tx_golden.py): the device build fills each frame's zeroed L4
+    checksum with the RFC's value, at every 16-B phase."""
+    import json
+    cases = json.load(open(os.path.join(HERE, "golden", "ip6_tx.json")))
+    frames = [bytes.fromhex(c["frame"]) for c in cases]
+    for lead in range(16):
+        hb = host_batch(frames, lead)
+        recs = oracle_recs(hb)
+        z = hb.frames.copy()
+        for i, c in enumerate(cases):
+            k = i + (1 if lead else 0)                       # after the lead junk frame
+            ck = int(hb.offsets[k]) + int(recs[k]["l4_off"]) + (6 if c["kind"] == "udp" else 16)
+            z[ck:ck + 2] = 0
+        hz = gen.HostBatch(hb.config, hb.n, hb.seed, z, hb.offsets, hb.stride, hb.frame_len)
+        db = engine.DeviceBatch.from_host(hz)
+        d = torch.from_numpy(np.ascontiguousarray(recs).view(np.uint8).copy()).cuda()
+        assert engine.build_batch(db, d, 3).cpu().numpy()[(1 if lead else 0):].all()
+        assert np.array_equal(db.frames.cpu().numpy()[:hb.frames.size], hb.frames)

@@ -302,3 +302,64 @@ def test_cursor_mut_positions_and_panics():
         c.advance(407)
         with pytest.raises(AssertionError):
             getattr(c, op)(10000)
+
+
+def test_ipv6_without_l4_view_leaves_caller_bytes():
+    """An IPv6 next_header of 17 with the UDP header written by the caller (move_back, no
+    Udp view): the build writes no L4 header over it (prepend_header leaves those bytes),
+    even with the L4 checksum fill requested; the next_header byte stays 17."""
+    udp = bytes([0x12, 0x34, 0x00, 0x35, 0x00, 0x10, 0xab, 0xcd])    # hand-made UDP header
+    pkt = tv.CursorMut(14 + 40 + 8 + 8)
+    pkt.advance(14 + 40 + 8)
+    buf = pkt
+    buf.move_back(8, udp)
+    ip = tv.Ipv6.prepend_header(buf)
+    ip.set_next_header(IpProtocol.UDP)
+    ip.set_hop_limit(9)
+    ip.set_src_addr("2001:db8::5")
+    ip.set_dst_addr("2001:db8::6")
+    eth = tv.EtherFrame.prepend_header(ip.release())
+    eth.set_ethertype(EtherType.IPV6)
+    rec, extra = eth.release().record()
+    b = ip6_block(np.array([rec]))[0]
+    assert int(rec["ip_protocol"]) == 59 and int(b["ip6_next_header"]) == 17
+    assert int(rec["l4_off"]) == 14 + 40 + 8 and int(b["ip6_n_ext"]) == 1
+    out, _, built, _ = build([(rec, extra)], [70], 3, [b"\x77" * 8])
+    assert built[0] == 1
+    f = bytes(out[:70])
+    assert f[54:62] == udp and f[20] == 17 and f[21] == 9 and f[62:70] == b"\x77" * 8
+
+
+def test_ipv4_udp_protocol_without_udp_view_is_refused():
+    """IPv4 protocol 17 with no Udp view: the record cannot say "leave the L4 bytes", so the
+    host view refuses it rather than let the build overwrite them."""
+    pkt = tv.CursorMut(14 + 20 + 8)
+    pkt.advance(14 + 20)
+    ip = tv.Ipv4.prepend_header(pkt, tv.IPV4_HEADER_TEMPLATE)
+    ip.set_protocol(IpProtocol.UDP)
+    eth = tv.EtherFrame.prepend_header(ip.release(), tv.ETHER_FRAME_HEADER_TEMPLATE)
+    eth.set_ethertype(EtherType.IPV4)
+    with pytest.raises(ValueError):
+        eth.release().record()
+
+
+def test_ipv6_build_checksums_match_rfc8200_fixture():
+    """The IPv6 build's L4 checksum fill against frames whose checksums were worked out
+    from RFC 8200 section 8.1 + RFC 1071 alone (tests/golden/make_ip6_tx_golden.py, no
+    engine or oracle code): each parses with a valid sum, and a build from its own parse
+    record with the checksum field zeroed writes it back byte for byte (the reference has no
+    IPv6 pseudo-header code: this pins the extension to the RFC, not to the oracle)."""
+    import json
+    cases = json.load(open(os.path.join(HERE, "golden", "ip6_tx.json")))
+    for c in cases:
+        f = bytes.fromhex(c["frame"])
+        r = oracle.parse_one(f, F6)
+        assert r["status"] == STATUS["OK"] and r["l4_sum"] == 0xffff, c["kind"]
+        assert int(r["l4_checksum"]) == c["checksum"]
+        z = bytearray(f)
+        ck = int(r["l4_off"]) + (6 if c["kind"] == "udp" else 16)
+        z[ck:ck + 2] = b"\0\0"
+        buf = np.frombuffer(bytes(z), np.uint8)
+        offs = np.array([0, len(f)], np.uint32)
+        out, built = oracle.build_batch(buf, 1, np.array([r]), 3, offsets=offs)
+        assert built[0] == 1 and bytes(out) == f, c
