@@ -14,6 +14,19 @@ pub const RPKT_REC_BYTES: usize = 80;
 pub const RPKT_REC16_BYTES: usize = 16;
 pub const RPKT_OPTS_BYTES: usize = 64;
 pub const RPKT_LAYERS_BYTES: usize = 64;
+pub const RPKT_TUN_BYTES: usize = 16;
+pub const RPKT_MAX_GTP_EXT: usize = 8;
+// enum rpkt_tun_kind / rpkt_tun_status
+pub const RPKT_TUN_NONE: u8 = 0;
+pub const RPKT_TUN_VXLAN: u8 = 1;
+pub const RPKT_TUN_GTPU: u8 = 2;
+pub const RPKT_TUN_GRE: u8 = 3;
+pub const RPKT_T_OK: u8 = 0;
+pub const RPKT_T_NONE: u8 = 1;
+pub const RPKT_T_BAD: u8 = 2;
+pub const RPKT_T_NOT_TPDU: u8 = 3;
+pub const RPKT_T_EXT_BAD: u8 = 4;
+pub const RPKT_T_INNER_UNKNOWN: u8 = 5;
 pub const RPKT_MAX_LAYERS: usize = 16;
 pub const RPKT_MAX_FIELD_REQS: u32 = 32;
 pub const RPKT_FLOW_MAX_BUCKETS: u32 = 65535;
@@ -39,6 +52,8 @@ pub const RPKT_S_IP6_BAD_LEN: u8 = 15;
 pub const RPKT_S_IP6_EXT_SHORT: u8 = 16;
 pub const RPKT_S_IP6_EXT_BAD_LEN: u8 = 17;
 pub const RPKT_S_IP6_FRAGMENT: u8 = 18;
+pub const RPKT_S_ICMP_EMPTY: u8 = 19;
+pub const RPKT_S_NO_INNER: u8 = 20;
 pub const RPKT_MAX_IP6_EXT: usize = 8;
 
 // enum rpkt_err
@@ -206,6 +221,22 @@ pub struct rpkt_opts_t {
 }
 const _: () = assert!(core::mem::size_of::<rpkt_opts_t>() == RPKT_OPTS_BYTES);
 
+/// One frame's tunnel (rpkt_gpu_parse_tunnel_batch), 16 bytes.
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
+pub struct rpkt_tun_t {
+    pub kind: u8,
+    pub status: u8,
+    pub tun_off: u16,
+    pub inner_off: u16,
+    pub inner_type: u16,
+    pub id: u32,
+    pub hdr0: u8,
+    pub hdr1: u8,
+    pub aux: u16,
+}
+const _: () = assert!(core::mem::size_of::<rpkt_tun_t>() == RPKT_TUN_BYTES);
+
 /// One frame's protocol stack from the pktfmt-derived walk, 64 bytes.
 #[repr(C)]
 #[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
@@ -311,6 +342,9 @@ extern "C" {
                                                 flow_ev_dev: *mut rpkt_flow_ev_t, n_buckets: u32,
                                                 stream: *mut c_void) -> c_int;
 
+    pub fn rpkt_gpu_parse_tunnel_batch(batch: *const rpkt_batch_t, flags: u32,
+                                       outer_dev: *mut rpkt_rec_t, tun_dev: *mut rpkt_tun_t,
+                                       inner_dev: *mut rpkt_rec_t, stream: *mut c_void) -> c_int;
     pub fn rpkt_gpu_layers_batch(batch: *const rpkt_batch_t, layers_dev: *mut rpkt_layers_t,
                                  stream: *mut c_void) -> c_int;
     pub fn rpkt_gpu_fields_batch(batch: *const rpkt_batch_t, layers_dev: *const rpkt_layers_t,

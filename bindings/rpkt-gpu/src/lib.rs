@@ -36,11 +36,11 @@ pub fn check(rc: i32) -> Result<(), Error> {
 
 /// The name of a per-frame status (`rpkt_gpu_status_name`).
 pub fn status_name(status: u8) -> &'static str {
-    const NAMES: [&str; 19] = ["OK", "ETH_SHORT", "VLAN_SHORT", "NOT_IPV4", "IP_SHORT",
+    const NAMES: [&str; 21] = ["OK", "ETH_SHORT", "VLAN_SHORT", "NOT_IPV4", "IP_SHORT",
                                "IP_BAD_IHL", "IP_IHL_GT_LEN", "IP_TOT_LT_IHL", "IP_TOT_GT_LEN",
                                "L4_OTHER", "UDP_SHORT", "UDP_BAD_LEN", "TCP_SHORT",
                                "TCP_BAD_DOFF", "IP6_SHORT", "IP6_BAD_LEN", "IP6_EXT_SHORT",
-                               "IP6_EXT_BAD_LEN", "IP6_FRAGMENT"];
+                               "IP6_EXT_BAD_LEN", "IP6_FRAGMENT", "ICMP_EMPTY", "NO_INNER"];
     NAMES.get(status as usize).copied().unwrap_or("?")
 }
 

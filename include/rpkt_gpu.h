@@ -66,8 +66,15 @@ enum rpkt_status {
                                    ipv6/generated.rs:243,386,530,698,852)          */
     RPKT_S_IP6_EXT_BAD_LEN = 17,/* extension header: header_len < min or > chunk_len
                                    (ipv6/generated.rs:248,391,535,857)             */
-    RPKT_S_IP6_FRAGMENT = 18    /* a Fragment header with offset != 0 or M set: the
+    RPKT_S_IP6_FRAGMENT = 18,   /* a Fragment header with offset != 0 or M set: the
                                    upper-layer header needs reassembly, not parsed */
+    RPKT_S_ICMP_EMPTY = 19,     /* IPv4 parsed, protocol 1 (ICMP), empty payload: the
+                                   reference's calculate_icmp_checksum panics on it
+                                   (icmp_data.len() - 1 underflows,
+                                   icmpv4/generated.rs:2684); otherwise as L4_OTHER */
+    RPKT_S_NO_INNER = 20        /* rpkt_gpu_parse_tunnel_batch's inner record of a frame
+                                   whose tunnel was not decoded (rpkt_tun_t.status != OK):
+                                   every other field 0 */
 };
 
 #define RPKT_MAX_VLAN 2
@@ -118,6 +125,20 @@ enum rpkt_flags {
  *   ip_sum             checksum::from_slice(ipv4[0..header_len]); 0xffff <=> valid
  *   l4_sum             checksum::combine(&[pseudo(src,dst,proto,l4_len),
  *                      from_slice(l4[0..l4_len])]); 0xffff <=> valid
+ *                      Status L4_OTHER (RPKT_F_L4_SUM), no pseudo header:
+ *                      - IPv4 protocol 1 (ICMP): from_slice over the whole IPv4 payload
+ *                        [l4_off, l3_off + packet_len); the reference's
+ *                        calculate_icmp_checksum (icmpv4/generated.rs:2678-2701) over the
+ *                        same bytes is !l4_sum, so 0xffff <=> it returns 0 (a valid
+ *                        message, icmpv4_test.rs:82-96); an empty payload is
+ *                        RPKT_S_ICMP_EMPTY, not summed;
+ *                      - protocol / next header 47 (GRE) with the checksum-present bit
+ *                        (byte 0 & 0x80, gre/generated.rs:55) and >= 4 payload bytes:
+ *                        from_slice over the GRE header and its payload (RFC 2784 section
+ *                        2.5; Gre::checksum, gre/generated.rs:239): 0xffff <=> valid.
+ *                      (These are the sums of the outer layer only: a frame whose l4_sum
+ *                      is one of them keeps status L4_OTHER, so the compact verdict bit 1
+ *                      and the flow event's bit 49 do not cover them.)
  * Fields of layers that were not reached are zero.  Sums not requested by the
  * flags, or whose layer did not parse, are zero.
  *
@@ -375,6 +396,84 @@ typedef struct rpkt_chains {
  * mbuf chain, mbuf.rs:346-382).  recs_dev n_chains * 80 B, 16-byte aligned. */
 int rpkt_gpu_parse_chains(const rpkt_chains_t* chains, uint32_t flags, rpkt_rec_t* recs_dev,
                           rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
+
+/* ---- Tunnels: the inner frame of VXLAN, GTP-U and GRE ------------------------- */
+
+/* rpkt_gpu_parse_tunnel_batch decodes one tunnel level after the outer parse, as the
+ * reference's receive loops chain the views (the dispatch is the caller's in rpkt):
+ *   VXLAN   Udp::payload -> Vxlan::parse (vxlan/generated.rs:32-39) -> payload() (advance 8)
+ *           -> EtherFrame::parse ... (rpkt/tests/vlan_mpls_tests.rs:224-251);
+ *   GTP-U   Udp::payload -> Gtpv1::parse (gtpv1/generated.rs:33-49) -> payload() (trim to
+ *           packet_len, advance header_len, :98-108) -> the extension headers named by
+ *           next_extention_header (ExtPduNumber, ExtUdpPort, ExtLongPduNumber,
+ *           ExtServiceClassIndicator, ExtContainer, NrUp / PduSessionUp::group_parse, each
+ *           its parse and payload()) -> Ipv4|Ipv6::parse (gtpv1_test.rs:199-231, 284-320,
+ *           468-505);
+ *   GRE     Ipv4|Ipv6::payload -> GreGroup::group_parse (gre/generated.rs:800-820) ->
+ *           Gre::payload() (advance header_len) -> Ipv4|Ipv6|EtherFrame::parse
+ *           (gre_test.rs:20-99).
+ * Dispatch: an outer frame that parsed OK as UDP with destination port 4789 (VXLAN) or
+ * 2152 (GTP-U), else with that source port; or an outer IPv4 (first fragment) / IPv6
+ * frame whose upper-layer protocol is 47 (status L4_OTHER).  GTP-U carries an inner
+ * packet only as a GTPv1 (version 1) G-PDU (message type 255), by the version nibble of
+ * its first byte (4 / 6).  GRE's protocol type selects 0x0800 IPv4, 0x86DD IPv6,
+ * 0x6558 Ethernet (transparent bridging).  IPv6 inner packets need RPKT_F_IPV6. */
+enum rpkt_tun_kind {
+    RPKT_TUN_NONE = 0,
+    RPKT_TUN_VXLAN = 1,
+    RPKT_TUN_GTPU = 2,
+    RPKT_TUN_GRE = 3
+};
+enum rpkt_tun_status {
+    RPKT_T_OK = 0,            /* tunnel decoded: the inner record holds the inner frame     */
+    RPKT_T_NONE = 1,          /* no tunnel dispatch on this frame (kind NONE)               */
+    RPKT_T_BAD = 2,           /* Vxlan::parse / Gtpv1::parse / GreGroup::group_parse Err     */
+    RPKT_T_NOT_TPDU = 3,      /* GTP: not a GTPv1 G-PDU (version != 1 or message != 255)    */
+    RPKT_T_EXT_BAD = 4,       /* GTP: an extension header's parse Err, an unknown next
+                                 extension type, or more than RPKT_MAX_GTP_EXT of them      */
+    RPKT_T_INNER_UNKNOWN = 5  /* the inner protocol is none of Ether / IPv4 / IPv6 (an
+                                 IPv6 one without RPKT_F_IPV6, an empty T-PDU, GRE for
+                                 PPTP's PPP payload): inner_type says what it is, or 0     */
+};
+#define RPKT_MAX_GTP_EXT 8
+
+/* One frame's tunnel, 16 bytes. */
+typedef struct rpkt_tun {
+    uint8_t  kind;       /*  0 enum rpkt_tun_kind                                     */
+    uint8_t  status;     /*  1 enum rpkt_tun_status                                   */
+    uint16_t tun_off;    /*  2 frame offset of the VXLAN / GTPv1 / GRE header           */
+    uint16_t inner_off;  /*  4 frame offset of the inner frame: the tunnel's payload()  */
+    uint16_t inner_type; /*  6 0x6558 (an Ethernet frame), 0x0800, 0x86DD; GRE: its
+                             protocol_type (0x880B for PPTP); GTP: 0 when the T-PDU's
+                             version nibble is not 4 / 6                                 */
+    uint32_t id;         /*  8 Vxlan::vni, Gtpv1::teid, Gre::key (0 without the K bit)  */
+    uint8_t  hdr0;       /* 12 header byte 0: VXLAN flags (gbp_extention, vni_present),
+                             GTPv1 version / protocol_type / E / S / PN, GRE C / R / K / S
+                             / recursion_control                                         */
+    uint8_t  hdr1;       /* 13 header byte 1: VXLAN dont_learn / policy_applied, GTPv1
+                             message_type, GRE flags / version                           */
+    uint16_t aux;        /* 14 Vxlan::group_id; Gtpv1::sequence (a 12-B header, else 0);
+                             Gre::checksum (C or R bit, else 0)                          */
+} rpkt_tun_t;
+
+#define RPKT_TUN_BYTES 16u
+
+/* Parse + verify a batch and decode one tunnel level per frame:
+ *   outer_dev[i]  the record rpkt_gpu_parse_batch writes for frame i with the same flags;
+ *   tun_dev[i]    its tunnel (kind NONE / status NONE when there is none);
+ *   inner_dev[i]  the record of the inner frame [inner_off, the tunnel payload's end):
+ *                 rpkt_gpu_parse_batch's record of those bytes (an inner IPv4 / IPv6
+ *                 packet is parsed from its IP header: ethertype = inner_type, n_vlan 0,
+ *                 MACs 0), with l3_off / l4_off / payload_off / ip6_pdst_off as offsets in
+ *                 the OUTER frame (rpkt's Cursor::cursor() of the inner views) and
+ *                 frame_len = the inner frame's length; status RPKT_S_NO_INNER (all else
+ *                 0) when tun_dev[i].status != RPKT_T_OK.
+ * flags: RPKT_F_IP_SUM, RPKT_F_L4_SUM, RPKT_F_IPV6, applied to both levels (no flow
+ * events).  Each byte is read from HBM about once: the outer L4 sum (UDP, or GRE with
+ * its checksum) reuses the inner L4 sum's stream over the bytes the two share.
+ * outer_dev / inner_dev n * 80 B, tun_dev n * 16 B, all 16-byte aligned. */
+int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* batch, uint32_t flags, rpkt_rec_t* outer_dev,
+                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev, void* stream);
 
 /* ---- TX side ---------------------------------------------------------------- */
 

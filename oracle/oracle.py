@@ -61,6 +61,8 @@ def lib():
         u8p = ctypes.POINTER(ctypes.c_uint8)
         L.oracle_from_slice.argtypes = [u8p, ctypes.c_size_t]
         L.oracle_from_slice.restype = ctypes.c_uint16
+        L.oracle_icmp_checksum.argtypes = [u8p, ctypes.c_size_t]
+        L.oracle_icmp_checksum.restype = ctypes.c_int
         L.oracle_combine.argtypes = [ctypes.POINTER(ctypes.c_uint16), ctypes.c_size_t]
         L.oracle_combine.restype = ctypes.c_uint16
         L.oracle_from_buf.argtypes = [ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t),
@@ -123,6 +125,11 @@ def lib():
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_options_batch.restype = None
+        L.oracle_tunnel_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]
+        L.oracle_tunnel_batch.restype = None
         L.oracle_layers_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_void_p]
@@ -144,6 +151,14 @@ def from_slice(data):
     b = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     b = np.ascontiguousarray(b, dtype=np.uint8)
     return int(lib().oracle_from_slice(b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), b.size))
+
+
+def icmp_checksum(data):
+    """rpkt/src/icmpv4/generated.rs:2678-2701 calculate_icmp_checksum restated; None for
+    the empty slice (where the reference panics)."""
+    b = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+    r = int(lib().oracle_icmp_checksum(b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), b.size))
+    return None if r < 0 else r
 
 
 def combine(words):
@@ -296,6 +311,26 @@ def options_batch(frames, n, recs, offsets=None, stride=0, frame_len=0):
     lib().oracle_options_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n,
                                _ptr(recs), _ptr(out))
     return out
+
+
+def tunnel_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_parse_tunnel_batch on the CPU: (outer records, rpkt_tun_t, inner records)."""
+    from rpkt_amd.records import REC_DTYPE, TUN_DTYPE
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    outer = np.zeros(n, dtype=REC_DTYPE)
+    tun = np.zeros(n, dtype=TUN_DTYPE)
+    inner = np.zeros(n, dtype=REC_DTYPE)
+    lib().oracle_tunnel_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n, flags,
+                              _ptr(outer), _ptr(tun), _ptr(inner))
+    return outer, tun, inner
+
+
+def tunnel_one(frame, flags=3):
+    """(outer record, rpkt_tun_t, inner record) of one frame."""
+    b = np.frombuffer(bytes(frame), dtype=np.uint8)
+    o, t, i = tunnel_batch(b, 1, flags, offsets=np.array([0, b.size], np.uint32))
+    return o[0], t[0], i[0]
 
 
 def layers_batch(frames, n, offsets=None, stride=0, frame_len=0):

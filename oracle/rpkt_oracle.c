@@ -214,7 +214,37 @@ static void oracle_parse_l4(cursor_t* buf, uint8_t proto, const uint8_t* src, co
         rec->status = RPKT_S_OK;
     } else {
         rec->status = RPKT_S_L4_OTHER;
+        size_t n = cur_remaining(buf);
+        const uint8_t* p = cur_chunk(buf);
+        if (!v6 && proto == 1) {
+            /* ICMP: calculate_icmp_checksum (icmpv4/generated.rs:2678-2701) over the IPv4
+             * payload is the complement of from_slice over it (oracle_icmp_checksum below,
+             * tests/test_oracle_golden.py); its `icmp_data.len() - 1` (:2684) panics on an
+             * empty payload: that is a status here */
+            if (n == 0) { rec->status = RPKT_S_ICMP_EMPTY; return; }
+            if (flags & RPKT_F_L4_SUM) rec->l4_sum = oracle_from_slice(p, n);
+        } else if (proto == 47 && n >= 4 && (p[0] & 0x80)) {
+            /* GRE with checksum_present (gre/generated.rs:55): RFC 2784 section 2.5, the
+             * sum over the GRE header and payload (Gre::checksum :239) */
+            if (flags & RPKT_F_L4_SUM) rec->l4_sum = oracle_from_slice(p, n);
+        }
     }
+}
+
+/* rpkt/src/icmpv4/generated.rs:2678-2701 calculate_icmp_checksum, restated line by line
+ * (big-endian words, odd byte << 8, `while (checksum >> 16) != 0` fold, `!checksum as
+ * u16`); returns -1 for the empty slice, where the reference's `len() - 1` panics. */
+int oracle_icmp_checksum(const uint8_t* d, size_t len) {
+    if (len == 0) return -1;
+    uint32_t checksum = 0;
+    size_t i = 0;
+    while (i < len - 1) {
+        checksum += ((uint32_t)d[i] << 8) | d[i + 1];
+        i += 2;
+    }
+    if (i < len) checksum += (uint32_t)d[i] << 8;
+    while ((checksum >> 16) != 0) checksum = (checksum & 0xFFFF) + (checksum >> 16);
+    return (uint16_t)~checksum;
 }
 
 static uint32_t fold_be32x4(const uint8_t* a) {
@@ -319,6 +349,8 @@ static void oracle_parse_ip6(cursor_t* buf, uint32_t flags, rpkt_rec_t* rec) {
     oracle_parse_l4(buf, nh, ip + 8, pdst, 1, flags, rec);
 }
 
+static void oracle_parse_ip4(cursor_t* bufp, uint32_t flags, rpkt_rec_t* rec);
+
 /* Parse one frame exactly as the reference chain would, filling `rec`.
  * Chain: benches/rpkt/rpkt_parse.rs:62-80 (Ether -> IPv4 -> UDP) generalised
  * with the VLAN/QinQ walk of rpkt/tests/vlan_mpls_tests.rs:96-108 and the TCP
@@ -355,7 +387,12 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
         return;
     }
     if (et != 0x0800) { rec->status = RPKT_S_NOT_IPV4; return; }   /* rpkt_parse.rs:66 */
+    oracle_parse_ip4(&buf, flags, rec);
+}
 
+/* The IPv4 chain from the cursor at the IPv4 header. */
+static void oracle_parse_ip4(cursor_t* bufp, uint32_t flags, rpkt_rec_t* rec) {
+    cursor_t buf = *bufp;
     /* Ipv4::parse, ipv4/generated.rs:35-51 */
     rec->l3_off = (uint16_t)buf.start;
     size_t chunk_len = cur_remaining(&buf);
@@ -392,6 +429,21 @@ void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags,
     oracle_parse_l4(&buf, ip[9], ip + 12, ip + 16, 0, flags, rec);
 }
 
+/* A frame that starts at its IP header (a tunnel's inner packet: GTP-U T-PDU, GRE over
+ * IPv4 / IPv6): Ipv4::parse or Ipv6::parse on the whole buffer, as gtpv1_test.rs:229 and
+ * gre_test.rs:44 call them.  The record is oracle_parse_one's with ethertype = et (the
+ * tunnel's dispatch value), no link layer (n_vlan 0, MACs 0), l3_off 0. */
+void oracle_parse_at_ip(const uint8_t* frame, uint32_t frame_len, uint32_t flags, uint16_t et,
+                        rpkt_rec_t* rec) {
+    memset(rec, 0, sizeof(*rec));
+    rec->frame_len = frame_len;
+    rec->ethertype = et;
+    cursor_t buf = {frame, 0, frame_len};
+    if (et == 0x86dd && (flags & RPKT_F_IPV6)) { oracle_parse_ip6(&buf, flags, rec); return; }
+    if (et != 0x0800) { rec->status = RPKT_S_NOT_IPV4; return; }
+    oracle_parse_ip4(&buf, flags, rec);
+}
+
 /* The dispatch ethertype (the one Ipv4/Ipv6::parse was chosen on) and whether the
  * record is an IPv6 record (include/rpkt_gpu.h: the IPv6 block). */
 static uint16_t rec_dispatch_et(const rpkt_rec_t* r) {
@@ -404,7 +456,8 @@ int oracle_rec_is_ip6(const rpkt_rec_t* r) {
 /* IPv4 header parsed (its sum and fields are valid) */
 int oracle_rec_ip4_parsed(const rpkt_rec_t* r) {
     return !oracle_rec_is_ip6(r) &&
-           (r->status == RPKT_S_OK || (r->status >= RPKT_S_L4_OTHER && r->status <= RPKT_S_TCP_BAD_DOFF));
+           (r->status == RPKT_S_OK || (r->status >= RPKT_S_L4_OTHER && r->status <= RPKT_S_TCP_BAD_DOFF) ||
+            r->status == RPKT_S_ICMP_EMPTY);
 }
 
 /* 5-tuple flow hash (shared definition with the device: include/rpkt_gpu.h). */

@@ -219,7 +219,16 @@ static void parse_pbuf_l4(pbuf_t* bufp, uint8_t proto, const uint8_t* src, const
         rec->payload_len = (uint16_t)pbuf_remaining(&buf);
         rec->status = RPKT_S_OK;
     } else {
+        /* ICMP / GRE-with-checksum sums over the IP payload (rpkt_oracle.c
+         * oracle_parse_l4), here from_buf over the segments */
         rec->status = RPKT_S_L4_OTHER;
+        uint64_t n = pbuf_remaining(&buf);
+        if (!v6 && proto == 1) {
+            if (n == 0) { rec->status = RPKT_S_ICMP_EMPTY; return; }
+            if (flags & RPKT_F_L4_SUM) rec->l4_sum = pbuf_from_buf(buf, n);
+        } else if (proto == 47 && n >= 4 && (pbuf_chunk(&buf)[0] & 0x80)) {
+            if (flags & RPKT_F_L4_SUM) rec->l4_sum = pbuf_from_buf(buf, n);
+        }
     }
 }
 

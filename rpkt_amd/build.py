@@ -24,8 +24,8 @@ ABLATE_LIB = os.path.join(OUT, "librpkt_gpu_ablate.so")
 GEN_LIB = os.path.join(OUT, "librpkt_gen.so")
 # the engine: one translation unit per kernel family, shared device code in rpkt_common.h
 GPU_SRC = [os.path.join(HERE, "csrc", f) for f in
-           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_abi.hip",
-            "rpkt_coll.hip")]
+           ("rpkt_parse.hip", "rpkt_tx.hip", "rpkt_walks.hip", "rpkt_fields.hip", "rpkt_tunnel.hip",
+            "rpkt_abi.hip", "rpkt_coll.hip")]
 GPU_DEPS = [os.path.join(HERE, "csrc", "rpkt_common.h"), os.path.join(HERE, "csrc", "rpkt_opts.h"),
             os.path.join(HERE, "csrc", "rpkt_proto_table.h")]        # included; the table is generated
 # units compiled a second time with other defines (same source: same unit hash)
@@ -42,6 +42,7 @@ UNIT_HEADERS = {"rpkt_parse.hip": ("rpkt_common.h", "rpkt_opts.h"),
                 "rpkt_tx.hip": ("rpkt_common.h",),
                 "rpkt_walks.hip": ("rpkt_common.h", "rpkt_opts.h", "rpkt_proto_table.h"),
                 "rpkt_fields.hip": ("rpkt_common.h",),
+                "rpkt_tunnel.hip": ("rpkt_common.h",),
                 "rpkt_abi.hip": ("rpkt_common.h",),
                 "rpkt_coll.hip": ("rpkt_common.h",)}
 # every unit has its header list (a unit added to GPU_SRC without one would make
@@ -80,7 +81,7 @@ def unit_hashes(defines=()):
     """Per-unit hashes (unit file + shared headers + compile switches), so a profile of one
     kernel family stays valid while another unit changes: "parse=... tx=... walks=..."."""
     return " ".join("%s=%s" % (u, source_hash(["rpkt_%s.hip" % u], defines))
-                    for u in ("parse", "tx", "walks", "fields"))
+                    for u in ("parse", "tx", "walks", "fields", "tunnel"))
 
 
 def build_gpu(force=False, extra=()):

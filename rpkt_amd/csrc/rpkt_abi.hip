@@ -28,7 +28,8 @@ const char* rpkt_gpu_status_name(int s) {
                                   "IP_BAD_IHL", "IP_IHL_GT_LEN", "IP_TOT_LT_IHL",
                                   "IP_TOT_GT_LEN", "L4_OTHER", "UDP_SHORT", "UDP_BAD_LEN",
                                   "TCP_SHORT", "TCP_BAD_DOFF", "IP6_SHORT", "IP6_BAD_LEN",
-                                  "IP6_EXT_SHORT", "IP6_EXT_BAD_LEN", "IP6_FRAGMENT"};
+                                  "IP6_EXT_SHORT", "IP6_EXT_BAD_LEN", "IP6_FRAGMENT",
+                                  "ICMP_EMPTY", "NO_INNER"};
     return (s >= 0 && s < (int)(sizeof(names) / sizeof(names[0]))) ? names[s] : "?";
 }
 

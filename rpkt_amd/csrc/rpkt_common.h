@@ -866,9 +866,14 @@ __device__ __forceinline__ uint32_t parse_ip6(const uint8_t* slot, uint32_t ph, 
 // Lane-per-frame parse from the LDS window: the rpkt chain with every getter, the
 // IPv4 header sum and the in-window part of the L4 sum.  Three dependent rounds of
 // LDS dword reads: link layer (bytes 0..23), IPv4 header at l3, L4 header at l4.
+// start_et != 0 (rpkt_gpu_parse_tunnel_batch's inner packets): the frame starts at its IP
+// header, dispatched as ethertype start_et (Ipv4|Ipv6::parse on the whole buffer); base:
+// added to every offset the record holds (the inner frame's position in the outer one).
+// Both are compile-time 0 for the other callers.
 __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame fr, bool valid,
                                            uint32_t flags, LaneRec& L,
-                                           __amdgpu_buffer_rsrc_t rs, uint32_t fb) {
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                           uint32_t start_et = 0u, uint32_t base = 0u) {
     const uint32_t ph = fr.off & 15u;
     const uint8_t* slot = &W.win[lane * kSlot];
     uint32_t* w = L.w;
@@ -881,48 +886,53 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     w[19] = len;
     uint32_t status = RPKT_S_OK;
 
-    // round 1: Ethernet + up to two 802.1Q/802.1ad tags, frame bytes [0, 24)
-    uint32_t E[6];
-    {
-        const uint32_t a0 = ph & ~3u, sh = ph & 3u;
-        uint32_t R[7];
+    uint32_t nvlan = 0, et = start_et;
+    if (start_et == 0u) {
+        // round 1: Ethernet + up to two 802.1Q/802.1ad tags, frame bytes [0, 24)
+        uint32_t E[6];
+        {
+            const uint32_t a0 = ph & ~3u, sh = ph & 3u;
+            uint32_t R[7];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) R[k] = lds32(slot, a0 + 4 * k);
+            for (int k = 0; k < 7; ++k) R[k] = lds32(slot, a0 + 4 * k);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) E[k] = align_bytes(R[k + 1], R[k], sh);
-    }
-    if (len < 14) {                                            // ether/generated.rs:36
-        L.status = RPKT_S_ETH_SHORT;
-        w[0] = RPKT_S_ETH_SHORT;
-        return;
-    }
-    w[1] = E[0];                                               // dst_addr, src_addr
-    w[2] = E[1];                                               //   ether/generated.rs:47-54
-    w[3] = E[2];
-    const uint32_t eth_et = be16_lo(E[3]);                     // ethertype :55-59
-    // VLAN walk (vlan/generated.rs:32-61), at most RPKT_MAX_VLAN tags
-    uint32_t nvlan = 0, et = eth_et;
-    if (is_tag(et)) {
-        if (len - 14 < 4) {
-            status = RPKT_S_VLAN_SHORT;
-        } else {
-            et = be16_lo(E[4]);
-            w[4] = be16_hi(E[3]);
-            w[5] = et;
-            nvlan = 1;
-            if (is_tag(et)) {
-                if (len - 18 < 4) {
-                    status = RPKT_S_VLAN_SHORT;
-                } else {
-                    et = be16_lo(E[5]);
-                    w[4] |= be16_hi(E[4]) << 16;
-                    w[5] |= et << 16;
-                    nvlan = 2;
+            for (int k = 0; k < 6; ++k) E[k] = align_bytes(R[k + 1], R[k], sh);
+        }
+        if (len < 14) {                                        // ether/generated.rs:36
+            L.status = RPKT_S_ETH_SHORT;
+            w[0] = RPKT_S_ETH_SHORT;
+            return;
+        }
+        w[1] = E[0];                                           // dst_addr, src_addr
+        w[2] = E[1];                                           //   ether/generated.rs:47-54
+        w[3] = E[2];
+        const uint32_t eth_et = be16_lo(E[3]);                 // ethertype :55-59
+        // VLAN walk (vlan/generated.rs:32-61), at most RPKT_MAX_VLAN tags
+        et = eth_et;
+        if (is_tag(et)) {
+            if (len - 14 < 4) {
+                status = RPKT_S_VLAN_SHORT;
+            } else {
+                et = be16_lo(E[4]);
+                w[4] = be16_hi(E[3]);
+                w[5] = et;
+                nvlan = 1;
+                if (is_tag(et)) {
+                    if (len - 18 < 4) {
+                        status = RPKT_S_VLAN_SHORT;
+                    } else {
+                        et = be16_lo(E[5]);
+                        w[4] |= be16_hi(E[4]) << 16;
+                        w[5] |= et << 16;
+                        nvlan = 2;
+                    }
                 }
             }
         }
+        w[0] = (nvlan << 8) | (eth_et << 16);
+    } else {
+        w[0] = start_et << 16;                                 // the tunnel's dispatch value
     }
-    w[0] = (nvlan << 8) | (eth_et << 16);
     // EtherType::IPV6 (ether/mod.rs), ipv6_test.rs:25: with RPKT_F_IPV6 only
     const bool v6 = (flags & RPKT_F_IPV6) && status == RPKT_S_OK && et == 0x86ddu;
     if (status == RPKT_S_OK && et != 0x0800u && !v6) status = RPKT_S_NOT_IPV4;
@@ -932,16 +942,17 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
         return;
     }
 
-    const uint32_t l3 = 14u + 4u * nvlan, rem = len - l3;
-    w[16] = l3;
+    const uint32_t l3 = start_et ? 0u : 14u + 4u * nvlan, rem = len - l3;
+    w[16] = base + l3;
     uint32_t l4, l4rem, proto, paddr;
     if (v6) {
         // round 2 (IPv6): the header, the extension headers, the pseudo header's addresses
         L.is6 = true;
         status = parse_ip6(slot, ph, fr, rs, fb, l3, rem, w, l4, l4rem, proto, paddr);
         if (status != RPKT_S_IP6_SHORT && status != RPKT_S_IP6_BAD_LEN) {
-            w[16] |= l4 << 16;
-            w[17] = (l4 & 0xffffu) | (l4rem << 16);
+            w[16] |= (base + l4) << 16;
+            w[17] = ((base + l4) & 0xffffu) | (l4rem << 16);
+            w[8] += base << 16;                                // ip6_pdst_off
         }
         if (status != RPKT_S_OK) {
             w[0] |= status;
@@ -976,8 +987,8 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
             w[18] = be_sum(raw_range_sum(slot, ip.R, ip.a0, ph + l3, ph + l3 + ihl4), fr.off + l3);
         l4 = l3 + ihl4;                                        // Ipv4::payload :115-127
         l4rem = tot - ihl4;
-        w[16] |= l4 << 16;
-        w[17] = l4 | (l4rem << 16);
+        w[16] |= (base + l4) << 16;
+        w[17] = (base + l4) | (l4rem << 16);
         // pseudo header (smoltcp pseudo_header_v4): src, dst
         paddr = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu);
     }
@@ -993,6 +1004,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
     if (v6 && __builtin_expect(ph + l4 + (proto == 17u ? 8u : 20u) > (uint32_t)kWin, 0))
         gread20(rs, fb, fr.off + l4, h4.F);
     uint32_t l4len = 0;
+    bool other_sum = false;                                    // ICMP / GRE: no pseudo header
     if (proto == 17u) {
         const uint32_t ulen = be16_lo(h4.F[1]);
         if (l4rem < 8) status = RPKT_S_UDP_SHORT;
@@ -1001,7 +1013,7 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
             w[11] = be16_lo(h4.F[0]) | (be16_hi(h4.F[0]) << 16);
             w[14] = ulen;
             w[15] = be16_hi(h4.F[1]);
-            w[17] = ((l4 + 8) & 0xffffu) | ((ulen - 8) << 16);   // Udp::payload :66-76
+            w[17] = ((base + l4 + 8) & 0xffffu) | ((ulen - 8) << 16);   // Udp::payload :66-76
             l4len = ulen;
         }
     } else if (proto == 6u) {
@@ -1014,19 +1026,30 @@ __device__ __forceinline__ void parse_lane(const WaveScratch& W, int lane, Frame
             w[13] = bswap32(h4.F[2]);
             w[14] = be16_lo(h4.F[3]) | (be16_hi(h4.F[3]) << 16);
             w[15] = be16_lo(h4.F[4]) | (be16_hi(h4.F[4]) << 16);
-            w[17] = ((l4 + hl) & 0xffffu) | ((l4rem - hl) << 16);   // Tcp::payload :125-131
+            w[17] = ((base + l4 + hl) & 0xffffu) | ((l4rem - hl) << 16);   // Tcp::payload :125-131
             l4len = l4rem;
         }
     } else {
         status = RPKT_S_L4_OTHER;
+        // ICMP (IPv4 protocol 1; calculate_icmp_checksum, icmpv4/generated.rs:2678-2701, is
+        // the complement of this sum; an empty payload panics there: ICMP_EMPTY) and GRE
+        // with checksum_present (gre/generated.rs:55; RFC 2784 section 2.5): the sum over
+        // the whole IP payload, no pseudo header (include/rpkt_gpu.h, l4_sum)
+        if (!v6 && proto == 1u) {
+            if (l4rem == 0u) status = RPKT_S_ICMP_EMPTY;
+            else other_sum = true;
+        } else if (proto == 47u && l4rem >= 4u && (h4.F[0] & 0x80u)) {
+            other_sum = true;
+        }
+        l4len = l4rem;
     }
     w[0] |= status;
     L.status = status;
-    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+    if ((status == RPKT_S_OK || other_sum) && (flags & RPKT_F_L4_SUM)) {
         L.want_l4 = true;
         // pseudo header: addresses, protocol, length (smoltcp pseudo_header_v4 / _v6; the
         // v6 u32 length is < 2^16 here, so one word)
-        L.pseudo = paddr + proto + l4len;
+        L.pseudo = other_sum ? 0u : paddr + proto + l4len;
         const uint32_t win_end = kWin - ph;                    // frame offset where LDS ends
         const uint32_t e = l4 + l4len;
         const uint32_t e_in = e < win_end ? e : win_end;
@@ -1047,7 +1070,8 @@ __device__ __forceinline__ uint64_t flow_event(const LaneRec& L, const uint32_t*
     uint32_t bucket = n_buckets;
     const uint32_t proto = (w[8] >> 8) & 0xffu;
     const bool ip4_parsed = !L.is6 && (L.status == RPKT_S_OK ||
-                                       (L.status >= RPKT_S_L4_OTHER && L.status <= RPKT_S_TCP_BAD_DOFF));
+                                       (L.status >= RPKT_S_L4_OTHER && L.status <= RPKT_S_TCP_BAD_DOFF) ||
+                                       L.status == RPKT_S_ICMP_EMPTY);
     // words 9 / 10: the IPv4 addresses, or the IPv6 address folds
     if (L.status == RPKT_S_OK)
         bucket = flow_hash(w[9], w[10], w[11] & 0xffffu, w[11] >> 16, proto) % n_buckets;

@@ -204,7 +204,12 @@ void build(const Spec& s, uint32_t len, uint8_t* out, Rng& r) {
             else put16(h4 + 4, r.chance(5000) ? r.below(8) : l4len + 1 + r.below(16));
             break;
         case 5: put16(ip + 2, r.below(ihl4)); break;                          // tot < ihl
-        case 7: { uint32_t p = r.below(256); ip[9] = (uint8_t)((p == 6 || p == 17) ? 47 : p); break; }
+        case 7: {                                                             // other protocol
+            uint32_t p = r.below(256);
+            ip[9] = (uint8_t)((p == 6 || p == 17) ? 47 : p);
+            if (r.below(8) == 0) { ip[9] = 1; put16(ip + 2, ihl4); }          // empty ICMP
+            break;
+        }
         case 8: put16(ip + 2, ihl4 + r.below(s.tcp ? 20 : 8)); break;          // L4 too short
         default: break;
     }
@@ -397,6 +402,137 @@ void build6(const Spec& s, uint32_t len, uint8_t* out, Rng& r) {
     memcpy(out, f, len);
 }
 
+// ---- tunnels (configs 13, 14): VXLAN, GTP-U with extension headers, GRE ----
+// The inner frame is built by build() / build6() (an inner IP packet: that frame without
+// its 14 Ethernet bytes), the tunnel and outer headers are prepended and the outer sums
+// stamped last (RFC 7348 VXLAN over UDP 4789, 3GPP TS 29.281 GTP-U over UDP 2152, RFC
+// 2784/2890 GRE), as rpkt's build side would (vlan_mpls_tests.rs:254-300,
+// gtpv1_test.rs:236-282, gre_test.rs:213-278).  fuzz: random tunnel-header faults.
+uint32_t put_ext(uint8_t* h, uint32_t type, uint32_t next, Rng& r) {
+    // one GTP-U extension header of `type`, its next type last; returns its length
+    uint32_t n;
+    switch (type) {
+        case 0x03: case 0x82: n = 8; break;                     // long PDU number
+        case 0x81: case 0x83: case 0x84: case 0x85: n = 4 * (1 + r.below(3)); break;
+        default: n = 4; break;                                  // 0x40 / 0xc0 / 0x20
+    }
+    h[0] = (uint8_t)(n / 4);
+    for (uint32_t k = 1; k + 1 < n; k++) h[k] = (uint8_t)r.next();
+    if (type == 0x84) h[1] = (uint8_t)((r.below(3) << 4) | (h[1] & 0xf));   // NrUp member
+    if (type == 0x85) h[1] = (uint8_t)((r.below(2) << 4) | (h[1] & 0xf));   // Dl / Ul
+    if (type == 0x84 && n < 8) { n = 8; h[0] = 2; for (uint32_t k = 2; k < 7; k++) h[k] = (uint8_t)r.next(); }
+    h[n - 1] = (uint8_t)next;
+    return n;
+}
+
+void build_tunnel(int config, uint32_t i, uint32_t len, uint8_t* out, Rng& r) {
+    static thread_local uint8_t f[(1u << 16) + 2048];
+    static const uint32_t kExtTypes[10] = {0xc0, 0x40, 0x20, 0x03, 0x82, 0x81, 0x83, 0x84, 0x85, 0xc0};
+    const bool fuzz = config == 14;
+    memset(f, 0, std::min<uint32_t>(len + 512, sizeof(f)));
+    const uint32_t kind = r.below(10) < 4 ? 1u : (r.below(6) < 4 ? 2u : 3u);   // VXLAN, GTP-U, GRE
+    // tunnel header bytes
+    uint8_t th[64];
+    uint32_t thl = 0, inner_eth = 0, gre_c = 0;
+    uint32_t gtp_len_at = 0;
+    if (kind == 1) {                                            // VXLAN: I flag, vni
+        th[0] = 0x08 | (r.below(2) ? 0x80 : 0); th[1] = (uint8_t)(r.below(2) ? 0x48 : 0);
+        put16(th + 2, r.below(65536)); put32(th + 4, (r.below(1u << 24)) << 8);
+        thl = 8; inner_eth = 1;
+    } else if (kind == 2) {                                     // GTP-U G-PDU, 0-3 extensions
+        const uint32_t n_ext = r.below(4);
+        const bool seq = r.below(2) == 1;
+        th[0] = (uint8_t)(0x30 | (n_ext ? 0x04 : 0) | (seq ? 0x02 : 0));
+        th[1] = 255;
+        put32(th + 4, (uint32_t)r.next());
+        thl = 8;
+        if (n_ext || seq) {
+            put16(th + 8, seq ? r.below(65536) : 0); th[10] = 0;
+            uint32_t types[4];
+            for (uint32_t k = 0; k < n_ext; k++) types[k] = kExtTypes[r.below(10)];
+            th[11] = (uint8_t)(n_ext ? types[0] : 0);
+            thl = 12;
+            for (uint32_t k = 0; k < n_ext; k++)
+                thl += put_ext(th + thl, types[k], k + 1 < n_ext ? types[k + 1] : 0, r);
+        }
+        gtp_len_at = 2;
+    } else {                                                    // GRE v0: C / K / S bits
+        const bool c = r.below(2) == 1, k = r.below(2) == 1, sq = r.below(4) == 0;
+        inner_eth = r.below(5) == 0;
+        th[0] = (uint8_t)((c ? 0x80 : 0) | (k ? 0x20 : 0) | (sq ? 0x10 : 0)); th[1] = 0;
+        put16(th + 2, inner_eth ? 0x6558 : 0x0800);
+        thl = 4;
+        if (c) { put32(th + thl, 0); gre_c = thl; thl += 4; }
+        if (k) { put32(th + thl, (uint32_t)r.next()); thl += 4; }
+        if (sq) { put32(th + thl, (uint32_t)r.next()); thl += 4; }
+    }
+    const uint32_t outer_l4 = 14 + 20;
+    const uint32_t tstart = outer_l4 + (kind == 3 ? 0 : 8);
+    const uint32_t istart = tstart + thl;
+    const uint32_t ilen = len > istart + 64 ? len - istart : 64;
+    // the inner frame: config 11's mix (IPv4 / IPv6 + extension headers, TCP / UDP)
+    {
+        static const uint8_t kExt6[5] = {0, 60, 43, 44, 51};
+        Spec si;
+        si.v6 = r.below(4) == 0;
+        si.tcp = r.below(2) == 1;
+        si.src = gen_ip(10, 1, 8192, r.below(8192)); si.dst = gen_ip(10, 2, 4096, i);
+        si.sport = 1024 + r.below(60000); si.dport = si.tcp ? 443 : 53;
+        si.rand_payload = true;
+        si.bad_ip = r.chance(100); si.bad_l4 = r.chance(100);
+        si.ident = i & 0xffff;
+        if (si.v6) { si.n_ext = (int)r.below(3); for (int k = 0; k < si.n_ext; k++) si.ext[k] = kExt6[r.below(5)]; }
+        if (fuzz) {
+            si.ihl = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            si.doff = r.below(4) == 0 ? 5 + (int)r.below(11) : 5;
+            si.fault = r.below(4) == 0 ? 2 + (int)r.below(7) : 0;
+        }
+        std::vector<uint8_t> tmp(ilen + 14 + 64);
+        if (si.v6) build6(si, inner_eth ? ilen : ilen + 14, tmp.data(), r);
+        else build(si, inner_eth ? ilen : ilen + 14, tmp.data(), r);
+        memcpy(f + istart, tmp.data() + (inner_eth ? 0 : 14), ilen);
+        if (!inner_eth && kind == 3 && si.v6) put16(th + 2, 0x86dd);
+    }
+    memcpy(f + tstart, th, thl);
+    const uint32_t total = istart + ilen;                       // == len unless len < istart + 64
+    // outer Ether + IPv4 (+ UDP)
+    memcpy(f, kDmac, 6); memcpy(f + 6, kSmac, 6); put16(f + 12, 0x0800);
+    uint8_t* ip = f + 14;
+    ip[0] = 0x45; ip[1] = 0; put16(ip + 2, total - 14); put16(ip + 4, i & 0xffff);
+    put16(ip + 6, 0x4000); ip[8] = 64; ip[9] = (uint8_t)(kind == 3 ? 47 : 17);
+    put32(ip + 12, gen_ip(172, 74, 8192, r.below(8192))); put32(ip + 16, kDip);
+    if (kind != 3) {
+        uint8_t* u = f + outer_l4;
+        put16(u, 1024 + r.below(60000)); put16(u + 2, kind == 1 ? 4789 : 2152);
+        put16(u + 4, total - outer_l4);
+        if (gtp_len_at) put16(f + tstart + 2, total - tstart - 8);   // GTP length
+        const bool zero = kind == 1 && r.below(2) == 0;         // VXLAN: RFC 7348 allows 0
+        uint32_t ps = ones_sum(ip + 12, 8, 0) + 17 + (total - outer_l4);
+        uint32_t ck = zero ? 0 : ((~ones_sum(u, total - outer_l4, ps)) & 0xffff);
+        if (!zero && ck == 0) ck = 0xffff;
+        if (!zero && r.chance(100)) { ck ^= 0x5a5a; if (ck == 0) ck = 1; }
+        put16(u + 6, ck);
+    } else if (th[0] & 0x80) {                                  // the GRE checksum
+        uint32_t ck = (~ones_sum(f + tstart, total - tstart, 0)) & 0xffff;
+        if (r.chance(100)) ck ^= 0x0101;
+        put16(f + tstart + gre_c, ck);
+    }
+    uint32_t ick = (~ones_sum(ip, 20)) & 0xffff;
+    if (r.chance(100)) ick ^= 0x00ff;
+    put16(ip + 10, ick);
+    if (fuzz) {                                                 // tunnel-header faults
+        switch (r.below(8)) {
+            case 0: f[tstart + r.below(thl)] = (uint8_t)r.next(); break;     // any header byte
+            case 1: if (kind == 2) put16(f + tstart + 2, r.below(65536)); break;   // GTP length
+            case 2: if (kind == 2 && thl > 12) f[tstart + 12 + r.below(thl - 12)] = (uint8_t)r.next(); break;
+            case 3: if (kind == 2) f[tstart + 1] = (uint8_t)r.below(256); break;  // message type
+            case 4: if (kind == 3) f[tstart + 1] = (uint8_t)r.below(8); break;    // GRE version
+            default: break;
+        }
+    }
+    memcpy(out, f, len);
+}
+
 // config: 1 bench_rpkt (1k x 64B UDP, rpkt_build.rs header values), 2 64B UDP,
 // 3 1500B TCP, 4 IMIX mixed, 5 VLAN/QinQ + options TCP, 6 fuzz (all statuses),
 // 10 / 11 dual stack 64 B / 1500 B, 12 dual-stack fuzz (every IPv4 and IPv6 status).
@@ -519,6 +655,16 @@ void fill_range(int config, uint64_t seed, uint64_t first, const uint32_t* offse
         uint32_t len = lens[i];
         uint64_t off = offsets ? offsets[i] : (uint64_t)i * stride;
         Spec s = spec_for(config, seed, (uint32_t)gi, len, r);
+        if (config == 13 || config == 14) {
+            if (config == 14 && r.below(8) == 0) {          // truncated tunnel frames
+                std::vector<uint8_t> tmp(len + 200);
+                build_tunnel(config, (uint32_t)gi, len + 200, tmp.data(), r);
+                memcpy(frames + off, tmp.data(), len);
+            } else {
+                build_tunnel(config, (uint32_t)gi, len, frames + off, r);
+            }
+            continue;
+        }
         if ((config == 6 || config == 8 || config == 12) && s.fault == 1) {
             // truncation: build a full frame then cut it at a random length
             uint32_t full = len + 64;
@@ -548,7 +694,8 @@ void rpkt_gen_lengths(int config, uint64_t seed, uint64_t first, uint32_t n, uin
         uint32_t L;
         switch (config) {
             case 1: case 2: case 10: L = 64; break;
-            case 3: case 11: L = 1500; break;
+            case 3: case 11: case 13: L = 1500; break;
+            case 14: L = r.below(8) == 0 ? 40 + r.below(80) : 100 + r.below(1419); break;
             case 4: { uint32_t k = r.below(12); L = k < 7 ? 64 : (k < 11 ? 570 : 1500); break; }
             case 5: L = 64 + r.below(1518 - 64 + 1); break;
             case 7: L = 8000; break;

@@ -147,7 +147,8 @@ __device__ __forceinline__ OptSlices opt_slices(uint32_t status, uint32_t proto,
                                                 uint32_t l4, uint32_t doff4, bool is6) {
     OptSlices S;
     S.ip_parsed = !is6 && (status == RPKT_S_OK ||
-                           (status >= RPKT_S_L4_OTHER && status <= RPKT_S_TCP_BAD_DOFF));
+                           (status >= RPKT_S_L4_OTHER && status <= RPKT_S_TCP_BAD_DOFF) ||
+                           status == RPKT_S_ICMP_EMPTY);
     S.tcp = status == RPKT_S_OK && proto == 6u;
     S.ip_lo = l3 + 20u;
     S.ip_hi = S.ip_parsed ? l4 : S.ip_lo;

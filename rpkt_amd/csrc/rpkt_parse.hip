@@ -605,6 +605,7 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
         gread20(rs, S.fb, ck4 ? ab4 : S.fb, h4.F);
     }
     uint32_t l4len = 0;
+    bool other_sum = false;                                    // ICMP / GRE (parse_lane)
     if (proto == 17u) {
         const uint32_t ulen = be16_lo(h4.F[1]);
         if (ck4 < 8) status = RPKT_S_UDP_SHORT;
@@ -630,13 +631,22 @@ __device__ __forceinline__ void parse_chain_lane(const WaveScratch& W, int lane,
             l4len = l4rem;
         }
     } else {
+        // ICMP and GRE-with-checksum sums over the IP payload, as parse_lane (the GRE
+        // header's first byte is the first byte of the chunk at l4)
         status = RPKT_S_L4_OTHER;
+        if (!v6 && proto == 1u) {
+            if (l4rem == 0u) status = RPKT_S_ICMP_EMPTY;
+            else other_sum = true;
+        } else if (proto == 47u && l4rem >= 4u && (h4.F[0] & 0x80u)) {
+            other_sum = true;
+        }
+        l4len = l4rem;
     }
     w[0] |= status;
     L.status = status;
-    if (status == RPKT_S_OK && (flags & RPKT_F_L4_SUM)) {
+    if ((status == RPKT_S_OK || other_sum) && (flags & RPKT_F_L4_SUM)) {
         L.want_l4 = true;
-        L.pseudo = paddr + proto + l4len;
+        L.pseudo = other_sum ? 0u : paddr + proto + l4len;
         const uint32_t e = l4 + l4len;
         L.l4_start_abs = s0.off + l4;                          // segment 0's byte phase
         if (fast4) {

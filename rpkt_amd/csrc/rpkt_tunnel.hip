@@ -1,0 +1,304 @@
+// rpkt_tunnel.hip — rpkt_gpu_parse_tunnel_batch: the outer parse, one tunnel level
+// (VXLAN, GTP-U with its extension headers, GRE) and the parse of the inner frame, with
+// every sum of both levels, in one pass per 64-frame tile (include/rpkt_gpu.h documents
+// the records and the dispatch; oracle/rpkt_oracle_tunnel.c restates it on the CPU).
+//
+// One wavefront per tile, as parse_kernel: the outer header windows go to LDS and each
+// lane runs parse_lane on its frame; the lane then decodes the tunnel header(s) from the
+// same window (FrameDw: global memory past it), the outer record is staged in a second
+// LDS area, the inner frames' header windows replace the outer ones (their lines were just
+// fetched: mostly L2 hits) and parse_lane runs again from the inner frame's first byte
+// (its IP header for GTP-U and GRE).  The L4 bytes past the inner windows are summed by
+// one flattened chunk stream (rpkt_common.h); the outer L4 sum (UDP, or GRE with its
+// checksum), whose range contains the inner one, takes the inner stream's sum for the
+// bytes they share and streams only the rest -- the bytes between the outer window and
+// the inner stream (inside the inner window's lines) and any trailer after the inner
+// packet -- so each payload byte leaves HBM about once for all four sums.
+#include "rpkt_common.h"
+
+namespace {
+
+struct Tunnel {
+    uint32_t w[4];      // rpkt_tun_t as 4 little-endian words
+    uint32_t is, ie;    // the inner frame, frame offsets [is, ie)
+    uint32_t start_et;  // the inner frame's first header: 0 Ethernet, 0x0800, 0x86DD
+    bool ok;
+};
+
+__device__ __forceinline__ void tun_set(Tunnel& T, uint32_t kind, uint32_t status, uint32_t tun_off,
+                                        uint32_t inner_off, uint32_t inner_type) {
+    T.w[0] = kind | (status << 8) | (tun_off << 16);
+    T.w[1] = (inner_off & 0xffffu) | (inner_type << 16);
+}
+
+// The inner packet of a GTP-U T-PDU or a GRE payload by its first header's type:
+// 0x0800 IPv4, 0x86DD IPv6 (with RPKT_F_IPV6), 0x6558 Ethernet; anything else is
+// INNER_UNKNOWN.
+__device__ __forceinline__ void tun_inner(Tunnel& T, uint32_t kind, uint32_t ts, uint32_t is,
+                                          uint32_t ie, uint32_t type, uint32_t flags) {
+    const bool eth = type == 0x6558u, ip4 = type == 0x0800u;
+    const bool ip6 = type == 0x86ddu && (flags & RPKT_F_IPV6);
+    T.ok = eth || ip4 || ip6;
+    T.start_et = eth ? 0u : type;
+    T.is = is;
+    T.ie = ie;
+    tun_set(T, kind, T.ok ? RPKT_T_OK : RPKT_T_INNER_UNKNOWN, ts, is, type);
+}
+
+// The tunnel of one parsed frame (L: its outer record; dw: its bytes, frame offsets).
+// Every byte read lies inside the span its parse tested ([ts, te) and the headers in it).
+__device__ __forceinline__ Tunnel decode_tunnel(const LaneRec& L, const FrameDw& dw,
+                                                uint32_t flags) {
+    Tunnel T;
+    T.w[0] = RPKT_TUN_NONE | (RPKT_T_NONE << 8);
+    T.w[1] = T.w[2] = T.w[3] = 0u;
+    T.is = T.ie = T.start_et = 0u;
+    T.ok = false;
+    const uint32_t* w = L.w;
+    const uint32_t proto = (w[8] >> 8) & 0xffu;              // ip_protocol (IPv4 and IPv6)
+    uint32_t kind = RPKT_TUN_NONE, ts = 0u, te = 0u;
+    if (L.status == RPKT_S_OK && proto == 17u) {
+        // Udp::payload() (udp/generated.rs:66-76): [payload_off, + payload_len)
+        const uint32_t dp = w[11] >> 16, sp = w[11] & 0xffffu;
+        const uint32_t port = (dp == 4789u || dp == 2152u) ? dp
+                            : ((sp == 4789u || sp == 2152u) ? sp : 0u);
+        if (port != 0u) {
+            kind = port == 4789u ? RPKT_TUN_VXLAN : RPKT_TUN_GTPU;
+            ts = w[17] & 0xffffu;
+            te = ts + (w[17] >> 16);
+        }
+    } else if (L.status == RPKT_S_L4_OTHER && proto == 47u &&
+               (L.is6 || ((w[7] >> 16) & 0x1fffu) == 0u)) {
+        // Ipv4|Ipv6::payload() of a first (or only) fragment: [l4_off, + payload_len)
+        kind = RPKT_TUN_GRE;
+        ts = w[16] >> 16;
+        te = ts + (w[17] >> 16);
+    }
+    if (kind == RPKT_TUN_NONE) return T;
+    const uint32_t cl = te - ts;                             // chunk() == remaining()
+    tun_set(T, kind, RPKT_T_BAD, ts, 0u, 0u);
+    if (kind == RPKT_TUN_VXLAN) {
+        // Vxlan::parse (vxlan/generated.rs:32-39): chunk_len >= 8; getters :44-87;
+        // payload() :91-96 advance 8 -> EtherFrame::parse (vlan_mpls_tests.rs:250)
+        if (cl < 8u) return T;
+        const uint32_t d0 = dw(ts), d1 = dw(ts + 4u);
+        T.w[2] = bswap32(d1) >> 8;                            // vni, bytes 4..6
+        T.w[3] = (d0 & 0xffffu) | (be16_hi(d0) << 16);        // flags bytes 0, 1; group_id
+        tun_inner(T, kind, ts, ts + 8u, te, 0x6558u, flags);
+        return T;
+    }
+    if (kind == RPKT_TUN_GTPU) {
+        // Gtpv1::parse (gtpv1/generated.rs:33-49): chunk_len >= 8, header_len (8, or 12
+        // with any of E/S/PN, :239-250) <= chunk_len, header_len <= packet_len (length +
+        // 8, :81-84) <= remaining
+        if (cl < 8u) return T;
+        const uint32_t d0 = dw(ts);
+        const uint32_t b0 = d0 & 0xffu, msg = (d0 >> 8) & 0xffu;
+        const uint32_t hl = (b0 & 7u) ? 12u : 8u;
+        const uint32_t plen = be16_hi(d0) + 8u;
+        if (hl > cl || plen < hl || plen > cl) return T;
+        const uint32_t d2 = hl == 12u ? dw(ts + 8u) : 0u;
+        T.w[2] = bswap32(dw(ts + 4u));                        // teid :74-76
+        T.w[3] = (d0 & 0xffffu) | (be16_lo(d2) << 16);        // byte 0, message_type; sequence
+        // payload() :98-108: trim to packet_len, advance header_len
+        uint32_t c = ts + hl;
+        const uint32_t end = ts + plen;
+        if ((b0 >> 5) != 1u || msg != 255u) {                 // not a GTPv1 G-PDU
+            tun_set(T, kind, RPKT_T_NOT_TPDU, ts, c, 0u);
+            return T;
+        }
+        // the extension headers (gtpv1_test.rs:222-229, 306-318, 494-503): the type named
+        // by the previous header's next_extention_header (Gtpv1::next_extention_header
+        // :275-278 reads byte 11), each its parse, header_len and payload() (advance)
+        uint32_t nx = (b0 & 4u) ? (d2 >> 24) : 0u;
+        for (int k = 0; k < RPKT_MAX_GTP_EXT && nx != 0u; ++k) {
+            const uint32_t rem = end - c, x = dw(c);
+            const uint32_t e0 = x & 0xffu, t = (x >> 12) & 0xfu;
+            uint32_t need, mn, ehl;
+            if (nx == 0x40u || nx == 0xc0u || nx == 0x20u) {
+                need = 4u; mn = 4u; ehl = 4u;                 // ExtUdpPort :336-341,
+            } else if (nx == 0x03u || nx == 0x82u) {          //   ExtPduNumber :461-466,
+                need = 8u; mn = 8u; ehl = 8u;                 //   ExtServiceClassIndicator
+            } else if (nx == 0x81u || nx == 0x83u) {          //   :747-752; ExtLongPduNumber
+                need = 1u; mn = 1u; ehl = e0 * 4u;            //   :587-592; ExtContainer
+            } else if (nx == 0x84u && t <= 2u) {              //   :880-892 (header_len :902);
+                need = 2u; mn = t == 0u ? 6u : (t == 1u ? 7u : 3u); ehl = e0 * 4u;  // NrUp
+            } else if (nx == 0x85u && t <= 1u) {              //   :2308-2320; PduSessionUp
+                need = 2u; mn = 3u; ehl = e0 * 4u;            //   :1507-1518
+            } else {
+                need = ~0u; mn = 0u; ehl = 0u;                // unknown type / group Err
+            }
+            if (rem < need || rem < mn || ehl < mn || ehl > rem) {
+                tun_set(T, kind, RPKT_T_EXT_BAD, ts, c, 0u);
+                return T;
+            }
+            nx = dw(c + ehl - 1u) & 0xffu;                    // next_extention_header: last byte
+            c += ehl;
+        }
+        if (nx != 0u) {
+            tun_set(T, kind, RPKT_T_EXT_BAD, ts, c, 0u);
+            return T;
+        }
+        // the T-PDU: Ipv4 / Ipv6 by its version nibble (gtpv1_test.rs:229)
+        const uint32_t v = c < end ? (dw(c) >> 4) & 0xfu : 0u;
+        tun_inner(T, kind, ts, c, end, v == 4u ? 0x0800u : (v == 6u ? 0x86ddu : 0u), flags);
+        return T;
+    }
+    // GreGroup::group_parse (gre/generated.rs:800-820): chunk >= 4; (C, R, K, version,
+    // protocol_type) == (0, 0, 1, 1, 0x880B) -> GreForPPTP::parse (:371-386), version 0 ->
+    // Gre::parse (:33-44, header_len gre/mod.rs:68-85), else Err
+    // (a header that fails its parse leaves id / hdr0 / hdr1 / aux 0)
+    if (cl < 4u) return T;
+    const uint32_t d0 = dw(ts);
+    const uint32_t b0 = d0 & 0xffu, b1 = (d0 >> 8) & 0xffu, pt = be16_hi(d0), ver = b1 & 7u;
+    if ((b0 & 0xe0u) == 0x20u && ver == 1u && pt == 0x880bu) {
+        if (cl < 8u) return T;
+        const uint32_t d1 = dw(ts + 4u);
+        const uint32_t phl = 8u + ((b0 & 0x10u) ? 4u : 0u) + ((b1 & 0x80u) ? 4u : 0u);
+        if (phl > cl || be16_lo(d1) + phl > cl) return T;     // payload_len + header_len
+        T.w[2] = bswap32(d1);                                 // payload_len, call_id
+        T.w[3] = d0 & 0xffffu;
+        tun_set(T, kind, RPKT_T_INNER_UNKNOWN, ts, ts + phl, pt);   // PPP, not IP
+        return T;
+    }
+    if (ver != 0u) return T;
+    const uint32_t cr = (b0 & 0xc0u) ? 4u : 0u;
+    const uint32_t hl = 4u + cr + ((b0 & 0x20u) ? 4u : 0u) + ((b0 & 0x10u) ? 4u : 0u);
+    if (hl > cl) return T;
+    T.w[3] = (d0 & 0xffffu) | (cr ? be16_lo(dw(ts + 4u)) << 16 : 0u);   // checksum :236-241
+    if (b0 & 0x20u) T.w[2] = bswap32(dw(ts + 4u + cr));        // key :260-267
+    tun_inner(T, kind, ts, ts + hl, te, pt, flags);           // payload() advance header_len
+    return T;
+}
+
+// Records staged at rl (stride 21 dwords) -> recs[p0 .. p0 + 64), 1-KiB wave stores.
+__device__ __forceinline__ void flush_stage(const uint32_t* rl, int lane, rpkt_rec_t* recs,
+                                            uint32_t p0, uint32_t n) {
+    wave_sync();
+    const uint32_t nrec = n - p0 < (uint32_t)kWave ? n - p0 : (uint32_t)kWave;
+    u32x4* out = reinterpret_cast<u32x4*>(recs + p0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t c = k * kWave + lane, r = c / 5, pc = c % 5;
+        const uint32_t* src = rl + r * 21 + pc * 4;
+        if (r < nrec) __builtin_nontemporal_store(u32x4{src[0], src[1], src[2], src[3]}, &out[c]);
+    }
+}
+
+template <bool L4>
+__device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
+                                            const uint8_t* __restrict__ frames, uint32_t fb,
+                                            const uint32_t* __restrict__ offsets, uint32_t stride,
+                                            uint32_t frame_len, uint32_t n, uint32_t flags,
+                                            rpkt_rec_t* __restrict__ outer, rpkt_tun_t* __restrict__ tun,
+                                            rpkt_rec_t* __restrict__ inner, uint32_t p0, int lane) {
+    const uint32_t i = p0 + lane;
+    const bool valid = i < n;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
+    const SpanSrc spans{offsets, stride, frame_len, fb, n};
+    // header-only batches read each line once: non-temporal window loads (as parse_tile)
+    constexpr int kWinAux = L4 ? 0 : 2;
+
+    // 1. the outer header windows -> LDS, the outer parse
+    const Frame fr = spans.get(i);
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue<kWinAux>(rs, fb, fr, lane, d, addr);
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    wave_sync();
+    LaneRec L;
+    parse_lane(W, lane, fr, valid, flags, L, rs, fb);
+
+    // 2. the tunnel, from the outer window
+    const Tunnel T = decode_tunnel(L, FrameDw{&W.win[lane * kSlot], fr.off & 15u, fr.off, fb, rs},
+                                   flags);
+
+    // 3. the outer record to its own stage; its L4 sum state kept for the streams
+#pragma unroll
+    for (int k = 0; k < 20; ++k) OS[lane * 21 + k] = L.w[k];
+    [[maybe_unused]] const uint32_t o_ss = L.stream_s, o_se = L.stream_e, o_part = L.l4_part;
+    [[maybe_unused]] const uint32_t o_abs = L.l4_start_abs, o_pseudo = L.pseudo;
+    [[maybe_unused]] const bool o_want = L.want_l4;
+
+    // 4. the inner header windows -> LDS (the outer ones are no longer read), inner parse
+    const Frame fi = T.ok ? Frame{fr.off + T.is, T.ie - T.is} : Frame{0u, 0u};
+    {
+        u32x4 d[kWinChunks];
+        uint32_t addr[kWinChunks];
+        const uint32_t fix = window_issue<kWinAux>(rs, fb, fi, lane, d, addr);
+        wave_sync();                                  // every lane done with its outer window
+        window_commit(W, rs, fb, d, addr, fix, lane);
+    }
+    wave_sync();
+    parse_lane(W, lane, fi, T.ok, flags, L, rs, fb, T.start_et, T.is);
+    if (!T.ok) {
+#pragma unroll
+        for (int k = 0; k < 20; ++k) L.w[k] = 0u;
+        L.w[0] = RPKT_S_NO_INNER;
+        L.want_l4 = false;
+        L.stream_s = L.stream_e = 0u;
+    }
+    stage_record(W, lane, L.w);
+
+    // 5. L4 bytes past the windows: the inner stream, then the outer range's other bytes
+    if constexpr (L4) {
+        const uint32_t sp_i = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
+        const bool shared = o_want && L.want_l4 && L.stream_e > L.stream_s &&
+                            L.stream_s >= o_ss && L.stream_e <= o_se;
+        const uint32_t x = shared ? L.stream_s : o_se, y = shared ? L.stream_e : o_se;
+        uint32_t sp_o = wave_stream_sum<2>(rs, fb, o_want ? o_ss : 0u, o_want ? x : 0u, W, lane);
+        sp_o += wave_stream_sum<2>(rs, fb, o_want ? y : 0u, o_want ? o_se : 0u, W, lane);
+        if (shared) sp_o += sp_i;
+        if (L.want_l4)
+            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + be_sum(L.l4_part + sp_i, L.l4_start_abs)) << 16;
+        if (o_want) OS[lane * 21 + 18] |= fold16(o_pseudo + be_sum(o_part + sp_o, o_abs)) << 16;
+    }
+
+    // 6. records: outer, inner (1-KiB wave stores from the stages), tunnel (16 B per lane)
+    flush_stage(OS, lane, outer, p0, n);
+    flush_stage(rec_stage(W), lane, inner, p0, n);
+    if (valid) __builtin_nontemporal_store(u32x4{T.w[0], T.w[1], T.w[2], T.w[3]},
+                                           reinterpret_cast<u32x4*>(tun) + i);
+}
+
+// One wave per workgroup (as the parse: a CU slot frees when its wave ends); the second
+// record stage (5376 B) puts a wave at 15.1 KB of LDS: 10 waves per CU
+template <bool L4>
+__global__ __launch_bounds__(kWave, 2)
+void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
+                   const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
+                   uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ outer,
+                   rpkt_tun_t* __restrict__ tun, rpkt_rec_t* __restrict__ inner) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch;
+    __shared__ __attribute__((aligned(16))) uint32_t ostage[kWave * 21];
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t p0 = blockIdx.x * kWave;
+    if (p0 >= n) return;                                          // wave-uniform exit
+    tunnel_tile<L4>(scratch, ostage, frames, fb, offsets, stride, frame_len, n, flags, outer, tun,
+                    inner, p0, lane);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* outer_dev,
+                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev, void* stream) {
+    if (!b) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_IPV6)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev || !outer_dev || !tun_dev || !inner_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)outer_dev | (uintptr_t)tun_dev | (uintptr_t)inner_dev) & 15u) return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t grid = (b->n + kWave - 1) / kWave;
+    auto k = (flags & RPKT_F_L4_SUM) ? tunnel_kernel<true> : tunnel_kernel<false>;
+    return launch(k, dim3(grid), dim3(kWave), 0, (hipStream_t)stream, b->frames_dev,
+                  (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags, outer_dev,
+                  tun_dev, inner_dev);
+}
+
+}  // extern "C"

@@ -60,7 +60,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
            "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact", "rpkt_gpu_coll_unique_id",
            "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy", "rpkt_gpu_comm_init_timeout",
-           "rpkt_gpu_comm_abort"]
+           "rpkt_gpu_comm_abort", "rpkt_gpu_parse_tunnel_batch"]
 COLL_ID_BYTES = 128
 
 _lib = None
@@ -133,6 +133,10 @@ def lib():
         L.rpkt_gpu_parse_options_batch.restype = ctypes.c_int
         L.rpkt_gpu_parse_options_batch_compact.argtypes = L.rpkt_gpu_parse_options_batch.argtypes
         L.rpkt_gpu_parse_options_batch_compact.restype = ctypes.c_int
+        L.rpkt_gpu_parse_tunnel_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_uint32,
+                                                  ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_parse_tunnel_batch.restype = ctypes.c_int
         L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.rpkt_gpu_layers_batch.restype = ctypes.c_int
@@ -255,6 +259,21 @@ def parse_batch(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=Non
                                     n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_batch")
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
+
+
+def parse_tunnel_batch(batch, flags=3, outer=None, tun=None, inner=None, stream=None):
+    """rpkt_gpu_parse_tunnel_batch: returns (outer records, rpkt_tun_t, inner records) as
+    uint8 tensors (n * 80, n * 16, n * 80 bytes)."""
+    torch = _torch()
+    dev = batch.frames.device
+    outer = alloc_records(batch.n, dev) if outer is None else outer
+    inner = alloc_records(batch.n, dev) if inner is None else inner
+    tun = torch.empty(batch.n * 16, dtype=torch.uint8, device=dev) if tun is None else tun
+    d = batch.desc()
+    rc = lib().rpkt_gpu_parse_tunnel_batch(ctypes.byref(d), flags, outer.data_ptr(),
+                                           tun.data_ptr(), inner.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_tunnel_batch")
+    return outer, tun, inner
 
 
 def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):

@@ -22,6 +22,14 @@ Config ids follow BASELINE.json `configs` (1-based like SURVEY.md §8d):
  12 dual-stack fuzz: every IPv4 and IPv6 status (truncation, bad payload_len, bad or
     short extension headers, non-atomic fragments, chains past RPKT_MAX_IP6_EXT,
     other upper-layer protocols, UDP checksum 0 over IPv6), packed
+ 13 tunnel mix, 1,048,576 x 1500 B, stride 1500: 40 % VXLAN (outer UDP checksum 0 or
+    set), 36 % GTP-U G-PDUs with 0-3 extension headers of every type the reference
+    parses, 24 % GRE v0 (checksum / key / sequence bits, IPv4 or transparent Ethernet
+    inside); inner IPv4 or IPv6 (+ extension headers), TCP or UDP; 1 % bad sums at
+    every level; parsed with rpkt_gpu_parse_tunnel_batch (RPKT_F_IPV6)
+ 14 tunnel fuzz: config 13's shapes at 40..1518 B with inner-frame faults, random
+    tunnel-header bytes, GTP lengths / message types / extension bytes, GRE
+    versions, truncations, packed
 """
 import ctypes
 import os
@@ -31,13 +39,16 @@ import numpy as np
 from .build import GEN_LIB, build_gen
 
 DEFAULT_N = {1: 1000, 2: 1 << 20, 3: 1 << 20, 4: 8 << 20, 5: 4 << 20, 6: 1 << 16,
-             7: 1 << 18, 8: 1 << 15, 9: 1 << 20, 10: 1 << 20, 11: 1 << 20, 12: 1 << 16}
-DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9, 10: 10, 11: 11, 12: 12}
-STRIDED = {1: 64, 2: 64, 3: 1500, 10: 64, 11: 1500}
+             7: 1 << 18, 8: 1 << 15, 9: 1 << 20, 10: 1 << 20, 11: 1 << 20, 12: 1 << 16,
+             13: 1 << 20, 14: 1 << 16}
+DEFAULT_SEED = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 7, 8: 8, 9: 9, 10: 10, 11: 11, 12: 12,
+                13: 13, 14: 14}
+STRIDED = {1: 64, 2: 64, 3: 1500, 10: 64, 11: 1500, 13: 1500}
 CHAINED = (7, 8)
 DUAL_STACK = (10, 11, 12)                                 # generated with IPv6 frames
 # config 2 = extract + IPv4 header sum; the dual-stack configs parse with RPKT_F_IPV6
-FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3, 10: 11, 11: 11, 12: 11}
+FLAGS = {1: 3, 2: 1, 3: 3, 4: 3, 5: 3, 6: 3, 7: 3, 8: 3, 10: 11, 11: 11, 12: 11, 13: 11, 14: 11}
+TUNNEL = (13, 14)                                         # tunnel mixes (VXLAN, GTP-U, GRE)
 MBUF_ROOM, MBUF_HEADROOM = 2048, 128                      # RTE_MBUF_DEFAULT_DATAROOM, headroom
 # header-boundary cut positions for the chain fuzz (Ether 14, tags 18/22, IPv4 +20..60, L4 +8/20)
 FUZZ_CUTS = (0, 1, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 26, 30, 33, 34, 35, 38,

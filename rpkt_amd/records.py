@@ -79,7 +79,7 @@ STATUS = {
     "IP_BAD_IHL": 5, "IP_IHL_GT_LEN": 6, "IP_TOT_LT_IHL": 7, "IP_TOT_GT_LEN": 8,
     "L4_OTHER": 9, "UDP_SHORT": 10, "UDP_BAD_LEN": 11, "TCP_SHORT": 12, "TCP_BAD_DOFF": 13,
     "IP6_SHORT": 14, "IP6_BAD_LEN": 15, "IP6_EXT_SHORT": 16, "IP6_EXT_BAD_LEN": 17,
-    "IP6_FRAGMENT": 18,
+    "IP6_FRAGMENT": 18, "ICMP_EMPTY": 19, "NO_INNER": 20,
 }
 STATUS_NAME = {v: k for k, v in STATUS.items()}
 
@@ -184,3 +184,23 @@ def flow_ev_fields(ev):
     ev = np.asarray(ev, dtype=np.uint64)
     return (ev & np.uint64(0xffffffff), (ev >> np.uint64(32)) & np.uint64(0xffff),
             (ev >> np.uint64(48)) & np.uint64(1), (ev >> np.uint64(49)) & np.uint64(1))
+
+
+TUN_BYTES = 16
+TUN_DTYPE = np.dtype([           # rpkt_tun_t (include/rpkt_gpu.h), 16 B
+    ("kind", "u1"), ("status", "u1"), ("tun_off", "<u2"), ("inner_off", "<u2"),
+    ("inner_type", "<u2"), ("id", "<u4"), ("hdr0", "u1"), ("hdr1", "u1"), ("aux", "<u2"),
+])
+assert TUN_DTYPE.itemsize == TUN_BYTES
+TUN_KIND = {"NONE": 0, "VXLAN": 1, "GTPU": 2, "GRE": 3}
+TUN_STATUS = {"OK": 0, "NONE": 1, "BAD": 2, "NOT_TPDU": 3, "EXT_BAD": 4, "INNER_UNKNOWN": 5}
+MAX_GTP_EXT = 8
+
+
+def as_tunnels(raw):
+    """View a uint8 buffer of n*16 bytes as rpkt_tun_t records."""
+    a = np.asarray(raw)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a.reshape(-1).view(TUN_DTYPE)
+

@@ -150,6 +150,8 @@ def chunk_model_status(frame, seg_lens):
             return STATUS["TCP_SHORT"]
         hl = (frame[l4 + 12] >> 4) * 4
         return STATUS["TCP_BAD_DOFF"] if hl < 20 or hl > ck else STATUS["OK"]
+    if proto == 1 and limit == l4:                    # an empty ICMP payload
+        return STATUS["ICMP_EMPTY"]
     return STATUS["L4_OTHER"]
 
 
@@ -210,7 +212,7 @@ def test_fuzz_chains_against_chunk_model():
                     assert np.array_equal(got[p][k], packed[p][k])
     # the fuzz must actually produce chains whose verdict differs from the frame's
     assert n_diff > 20
-    assert len(set(got["status"].tolist())) == 14
+    assert len(set(got["status"].tolist())) == 15
 
 
 def test_chain_edge_cases():

@@ -287,3 +287,54 @@ def test_cursor_positions_and_panics():
     c = views.Packet(rec, b)
     c.advance(0)
     assert not views.EtherFrame.parse(c).is_ok()          # a moved cursor is no parse start
+
+
+def test_icmp_checksum_kat_and_relation_to_from_slice():
+    """rpkt/tests/icmpv4_test.rs:82-96: the Echo Request's checksum is non-zero, and the
+    message carrying it checks to 0.  calculate_icmp_checksum(d) == !from_slice(d) on any
+    non-empty slice (so a record's ICMP l4_sum of 0xffff <=> the reference's check returns
+    0), and the empty slice, where the reference panics, is refused."""
+    import numpy as np
+    data = bytearray([0x08, 0x00, 0x00, 0x00, 0x12, 0x34, 0x00, 0x01])
+    ck = oracle.icmp_checksum(data)
+    assert ck != 0
+    data[2], data[3] = ck >> 8, ck & 0xff
+    assert oracle.icmp_checksum(data) == 0
+    assert oracle.from_slice(bytes(data)) == 0xffff
+    assert oracle.icmp_checksum(b"") is None
+    rng = np.random.default_rng(11)
+    for n in list(range(1, 40)) + [1499, 1500, 65535]:
+        for _ in range(3):
+            d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            assert oracle.icmp_checksum(d) == (~oracle.from_slice(d)) & 0xffff, n
+    assert oracle.icmp_checksum(b"\xff" * 4) == 0 and oracle.icmp_checksum(b"\0" * 6) == 0xffff
+
+
+def test_icmp_and_gre_sums_in_records():
+    """IPv4 protocol 1 and GRE-with-checksum frames (status L4_OTHER) carry the sum of
+    their IP payload in l4_sum under RPKT_F_L4_SUM: the reference's ICMP captures
+    (ipv4_test.rs IPv4Option1/2/6/7) and GREv0_1 (checksum 30719, gre_test.rs:35-41) and
+    GREv0_3 verify as 0xffff; GRE without the C bit and every frame without the flag carry
+    0; an empty ICMP payload is RPKT_S_ICMP_EMPTY."""
+    for name in ("IPv4Option1.dat", "IPv4Option2.dat", "IPv4Option6.dat", "IPv4Option7.dat",
+                 "GREv0_1.dat", "GREv0_3.dat"):
+        f = oracle.load_dat(os.path.join(PKTS, name))
+        r = oracle.parse_one(f, flags=3)
+        assert int(r["status"]) == STATUS["L4_OTHER"] and int(r["l4_sum"]) == 0xffff, name
+        assert int(oracle.parse_one(f, flags=1)["l4_sum"]) == 0
+        if int(r["ip_protocol"]) == 1:
+            msg = f[int(r["l4_off"]):int(r["l3_off"]) + int(r["ip_packet_len"])]
+            assert oracle.icmp_checksum(msg) == 0, name
+    g = oracle.load_dat(os.path.join(PKTS, "GREv0_1.dat"))
+    gre = g[int(oracle.parse_one(g, 3)["l4_off"]):]
+    assert (gre[4] << 8) | gre[5] == 30719                     # gre_test.rs:41
+    for name in ("GREv0_2.dat", "GREv0_4.dat", "GREv1_1.dat"):   # no checksum_present
+        r = oracle.parse_one(oracle.load_dat(os.path.join(PKTS, name)), flags=3)
+        assert int(r["l4_sum"]) == 0, name
+    # an ICMP packet of just its IPv4 header: the empty message
+    f = bytearray(oracle.load_dat(os.path.join(PKTS, "IPv4Option6.dat")))
+    ihl = (f[14] & 0xf) * 4
+    f[16:18] = ihl.to_bytes(2, "big")
+    r = oracle.parse_one(bytes(f[:14 + ihl]), flags=3)
+    assert int(r["status"]) == STATUS["ICMP_EMPTY"] and int(r["l4_sum"]) == 0
+    assert int(r["ip_ttl"]) == 64 and int(r["l4_off"]) == 14 + ihl
