@@ -51,7 +51,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from rpkt_amd import dist as rdist, engine, fields, gen  # noqa: E402
-from rpkt_amd.records import (LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, F_IPV6,  # noqa: E402
+from rpkt_amd.records import (as_tunnels, LAYERS_DTYPE, REC_BYTES, REC16_BYTES, F_FLOW_EV, F_IPV6,  # noqa: E402
                               as_records, is_ip6)
 
 METRIC = "Mpps + GB/s device-resident parse+cksum, 64B & 1500B pkts, 1/2/4/8 MI355X"
@@ -320,7 +320,7 @@ def pmc_traffic_tx(leg, n=None):
     except (OSError, ValueError):
         return None, None
     unit = {"build": "tx", "forward": "tx", "opts": "walks", "optsc": "walks", "layers": "walks",
-            "fields": "fields"}[leg.rstrip("0123456789")]
+            "fields": "fields", "tunnel": "tunnel", "encap": "tx"}[leg.rstrip("0123456789")]
     if leg not in t["legs"] or not same_unit(t["legs"][leg].get("engine_build", t.get("engine_build")),
                                              unit):
         return None, None
@@ -904,7 +904,7 @@ FIELD_LEG = [("ETHER_ETHERFRAME", "dst_addr"), ("ETHER_ETHERFRAME", "src_addr"),
              ("TCP_TCP", "seq_num"), ("VXLAN_VXLAN", "vni")]
 
 
-TX_MODES = ("build", "forward", "opts", "optsc", "layers", "fields")
+TX_MODES = ("build", "forward", "opts", "optsc", "layers", "fields", "tunnel", "encap")
 
 
 def tx_legs(spec):
@@ -945,6 +945,12 @@ def run_tx(cfg, mode, args, rank, world):
     recs16 = [engine.parse_batch_compact(db, 3) for db in dbs] if mode == "optsc" else None
     outs = [torch.empty(hb.n * (64 if mode in ("opts", "optsc", "layers") else 1), dtype=torch.uint8,
                         device="cuda") for hb in hbs]
+    if mode == "encap":                        # the tunnel parse's outer + tunnel records
+        tpar = [engine.parse_tunnel_batch(db, pflags)[:2] for db in dbs]
+    if mode == "tunnel":                       # outer records, tunnels, inner records
+        outs = [(torch.empty(hb.n * REC_BYTES, dtype=torch.uint8, device="cuda"),
+                 torch.empty(hb.n * 16, dtype=torch.uint8, device="cuda"),
+                 torch.empty(hb.n * REC_BYTES, dtype=torch.uint8, device="cuda")) for hb in hbs]
     if mode == "fields":                       # the walk once, outside the timed region
         lays = [engine.layers_batch(db) for db in dbs]
         reqs = fields.requests(FIELD_LEG)
@@ -968,6 +974,12 @@ def run_tx(cfg, mode, args, rank, world):
         elif mode == "fields":
             engine.fields_batch(dbs[j], lays[j], reqs, values=vals[j], present=pres[j],
                                 stream=stream)
+        elif mode == "tunnel":
+            o, t, i = outs[j]
+            engine.parse_tunnel_batch(dbs[j], pflags, outer=o, tun=t, inner=i, stream=stream)
+        elif mode == "encap":
+            engine.build_tunnel_batch(dbs[j], tpar[j][0], tpar[j][1], 3, built=outs[j],
+                                      stream=stream)
         else:
             engine.forward_batch(dbs[j], dmac, smac, forbid, keep=outs[j], stream=stream,
                                  flags=fwd_flags)
@@ -1002,6 +1014,16 @@ def run_tx(cfg, mode, args, rank, world):
         np.arange(hbs[0].n, dtype=np.int64) * hbs[0].stride
     if mode == "build":
         alg = int(lens.sum()) + hbs[0].n * REC_BYTES + int(fixed.sum())
+    elif mode == "tunnel":                     # every frame byte once + 80 + 16 + 80 B written
+        alg = int(lens.sum()) + hbs[0].n * (2 * REC_BYTES + 16)
+    elif mode == "encap":                      # records read, the frame read once (sums), the
+        tr = as_tunnels(tpar[0][1].cpu().numpy())   # headers up to the tunnel header's end written
+        h0 = tr["hdr0"].astype(np.int64)
+        thl = np.select([tr["kind"] == 1, tr["kind"] == 2],
+                        [8, np.where(h0 & 7, 12, 8)],
+                        4 + 4 * ((h0 & 0xc0) != 0) + 4 * ((h0 & 0x20) != 0) + 4 * ((h0 & 0x10) != 0))
+        alg = int(lens.sum()) + hbs[0].n * (REC_BYTES + 16) + \
+            int((tr["tun_off"].astype(np.int64) + thl).sum())
     elif mode == "layers":                       # header bytes walked + 64 B out per frame
         lo = outs[0].cpu().numpy().view(LAYERS_DTYPE)
         walked = np.minimum(lo["payload_off"].astype(np.int64), lens)
@@ -1046,7 +1068,7 @@ def run_tx(cfg, mode, args, rank, world):
                             np.where(ip6_walked, fo + l3 + 40, 0)]),
             np.concatenate([np.where(ip_parsed, fo + l4, 0), np.where(tcp, fo + po, 0),
                             np.where(ip6_walked, fo + l4, 0)]))
-    else:
+    elif mode == "forward":
         kept = outs[0].cpu().numpy().astype(bool)
         # rewritten bytes of a kept frame: 0 .. l4 + 8 (IPv4: 42; IPv6: 62 and up)
         alg = int(lens.sum()) + hbs[0].n + int((r["l4_off"][kept].astype(np.int64) + 8).sum())
@@ -1070,6 +1092,10 @@ def run_tx(cfg, mode, args, rank, world):
                      if mode == "layers" else
                      "fields: %d pktfmt getters per frame over the layer walk (captures mix)"
                      % len(FIELD_LEG) if mode == "fields" else
+                     "tunnel: outer parse + VXLAN / GTP-U / GRE decode + inner parse, all four "
+                     "sums (rpkt_gpu_parse_tunnel_batch)" if mode == "tunnel" else
+                     "encap: outer headers + VXLAN / GTP-U / GRE header + IPv4, UDP and GRE "
+                     "checksum fill (rpkt_gpu_build_tunnel_batch)" if mode == "encap" else
                      "forward: loopback_rx firewall fused (parse + both sums, 8 forbidden "
                      "sources, swap + ttl-1 + MACs + checksum update)")}
 
@@ -1189,7 +1215,7 @@ def write_detail(path, main_res, extra, args, world, engine_build):
 # the headline, config 4's sharded parse + counter reduce, and the strong-scaling legs)
 LEG_DEFAULTS = {"also": ("3,4,5,7,10,11", "4"),
                 "tx": ("build2,build3,build11,forward2,forward10,opts5,optsc5,opts11,layers9,"
-                       "fields9", ""),
+                       "fields9,tunnel13,encap13", ""),
                 "compact": ("2,3", ""), "strong": ("2,3", "2,3"), "opts": ("5", ""),
                 "ring": ("2,10", "")}
 

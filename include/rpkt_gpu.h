@@ -499,6 +499,34 @@ int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* batch, uint32_t flags, rpkt_
 int rpkt_gpu_build_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev, uint32_t flags,
                          uint8_t* built_dev, void* stream);
 
+/* Encapsulation build: rpkt_gpu_build_batch plus, for each frame whose tun_dev[i].kind is
+ * not RPKT_TUN_NONE, the tunnel header written first, inside-out as the reference builds
+ * these frames (the inner frame, and a GTP-U frame's extension headers, are payload already
+ * in place):
+ *   VXLAN  Vxlan::prepend_header + set_gbp_extention / set_vni_present / set_dont_learn /
+ *          set_policy_applied (hdr0, hdr1) + set_group_id (aux) + set_vni (id), at the
+ *          outer UDP payload (l4 + 8; the record's protocol must be 17), byte 7 0
+ *          (vxlan/generated.rs:99-150; vlan_mpls_tests.rs:254-300);
+ *   GTP-U  Gtpv1::prepend_header(header of hdr0, hdr1) (length = remaining - 8) + set_teid
+ *          (id), and for a 12-B header (any of E/S/PN in hdr0) set_sequence (aux); bytes
+ *          10-11 (npdu, next_extention_header) are left as the buffer holds them, as the
+ *          extension headers after them (gtpv1/generated.rs:110-170, 254-310;
+ *          gtpv1_test.rs:236-282);
+ *   GRE    Gre::prepend_header(hdr0, hdr1) + set_protocol_type (inner_type), with a
+ *          checksum word (C or R) = aux, or with RPKT_BUILD_L4_CSUM and the C bit the RFC
+ *          2784 checksum over the GRE header and payload; a key word (K) = id; offset and
+ *          sequence words left as the buffer holds them; at l4 (protocol 47)
+ *          (gre/generated.rs:95-267; gre_test.rs:213-278).
+ * The outer UDP checksum fill then covers the tunnel header.  status, tun_off and inner_off
+ * are not read.  A frame whose tunnel header does not end within the frame and within
+ * its first RPKT_TUN_BUILD_MAX_END bytes (the header window at any 16-B phase: every IPv4
+ * outer frame and IPv6 ones with short extension chains), or does not match the record's
+ * protocol, is left untouched (built 0).  tun_dev n * 16 B, 16-byte aligned. */
+#define RPKT_TUN_BUILD_MAX_END 113u
+int rpkt_gpu_build_tunnel_batch(const rpkt_batch_t* batch, const rpkt_rec_t* recs_dev,
+                                const rpkt_tun_t* tun_dev, uint32_t flags, uint8_t* built_dev,
+                                void* stream);
+
 /* Firewall forward (rpkt-dpdk/examples/loopback_rx.rs:96-140), one fused pass per
  * frame: the parse chain of rpkt_gpu_parse_batch with both sums, then frame i is
  * forwarded when it is an untagged IPv4/UDP frame that parsed OK with a valid IPv4

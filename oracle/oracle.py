@@ -115,6 +115,11 @@ def lib():
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                          ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
         L.oracle_build_batch.restype = None
+        L.oracle_build_tunnel_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                ctypes.c_void_p]
+        L.oracle_build_tunnel_batch.restype = None
         L.oracle_forward_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -280,6 +285,18 @@ def build_batch(frames, n, recs, flags=3, offsets=None, stride=0, frame_len=0):
     built = np.zeros(n, dtype=np.uint8)
     lib().oracle_build_batch(_ptr(out), out.size, _ptr(offs), stride, frame_len, n, _ptr(recs),
                              flags, _ptr(built))
+    return out, built
+
+
+def build_tunnel_batch(frames, n, recs, tun, flags=3, offsets=None, stride=0, frame_len=0):
+    """rpkt_gpu_build_tunnel_batch on the CPU: returns (new frames buffer, built flags)."""
+    out = np.array(frames, dtype=np.uint8, copy=True)
+    recs = np.ascontiguousarray(recs)
+    tun = np.ascontiguousarray(tun)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    built = np.zeros(n, dtype=np.uint8)
+    lib().oracle_build_tunnel_batch(_ptr(out), out.size, _ptr(offs), stride, frame_len, n,
+                                    _ptr(recs), _ptr(tun), flags, _ptr(built))
     return out, built
 
 

@@ -210,6 +210,62 @@ int oracle_build_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, uint32_t fla
     return 1;
 }
 
+/* The encapsulation build (rpkt_gpu_build_tunnel_batch): the tunnel header written first
+ * at the outer UDP payload (VXLAN, GTP-U) or at l4 (GRE), as the reference's build tests
+ * prepend it before the outer headers (vlan_mpls_tests.rs:254-300, gtpv1_test.rs:236-282,
+ * gre_test.rs:213-278), then oracle_build_one (whose UDP checksum fill covers it), then a
+ * GRE checksum fill.  Templates: VXLAN_HEADER_TEMPLATE all zero (vxlan/generated.rs:12),
+ * GTPV1_HEADER_TEMPLATE, the GRE template; the setter values from the rpkt_tun_t. */
+int oracle_build_tunnel_one(uint8_t* f, uint32_t len, const rpkt_rec_t* r, const rpkt_tun_t* t,
+                            uint32_t flags) {
+    if (t->kind == RPKT_TUN_NONE) return oracle_build_one(f, len, r, flags);
+    if (t->kind > RPKT_TUN_GRE || r->n_vlan > RPKT_MAX_VLAN) return 0;
+    const uint32_t l3 = 14 + 4 * (uint32_t)r->n_vlan;
+    const uint32_t l4 = oracle_rec_is_ip6(r) ? r->l4_off : l3 + (uint32_t)(r->ip_vhl & 0xf) * 4;
+    const uint32_t h0 = t->hdr0;
+    uint32_t ts, hl;
+    if (t->kind == RPKT_TUN_GRE) {
+        if (r->ip_protocol != 47) return 0;
+        ts = l4;
+        hl = 4 + ((h0 & 0xc0) ? 4 : 0) + ((h0 & 0x20) ? 4 : 0) + ((h0 & 0x10) ? 4 : 0);  /* gre/mod.rs:68-85 */
+    } else {
+        if (r->ip_protocol != 17) return 0;
+        ts = l4 + 8;                                        /* Udp::payload */
+        hl = t->kind == RPKT_TUN_VXLAN ? 8 : ((h0 & 7) ? 12 : 8);   /* Gtpv1::header_len :239-250 */
+    }
+    if (ts + hl > len || ts + hl > RPKT_TUN_BUILD_MAX_END) return 0;
+    if (t->kind == RPKT_TUN_GTPU && len - ts > 65543) return 0;     /* gtpv1/generated.rs:116 */
+    uint8_t tmp[65536 + 16];
+    if (len > sizeof(tmp)) return 0;
+    memcpy(tmp, f, len);
+    uint8_t* h = tmp + ts;
+    const int gre_fill = t->kind == RPKT_TUN_GRE && (flags & RPKT_BUILD_L4_CSUM) && (h0 & 0x80);
+    if (t->kind == RPKT_TUN_VXLAN) {
+        memset(h, 0, 8);                                    /* Vxlan::prepend_header :99-105 */
+        h[0] = t->hdr0;                                     /* set_gbp_extention, set_vni_present .. */
+        h[1] = t->hdr1;                                     /* set_dont_learn, set_policy_applied .. */
+        put16(h + 2, t->aux);                               /* set_group_id */
+        h[4] = (uint8_t)(t->id >> 16); h[5] = (uint8_t)(t->id >> 8); h[6] = (uint8_t)t->id;  /* set_vni */
+    } else if (t->kind == RPKT_TUN_GTPU) {
+        h[0] = t->hdr0;                                     /* Gtpv1::prepend_header :112-122: */
+        h[1] = t->hdr1;                                     /*   the 8-B header given, then */
+        put16(h + 2, len - ts - 8);                         /*   set_packet_len(remaining) */
+        put32(h + 4, t->id);                                /* set_teid :160 */
+        if (hl == 12) put16(h + 8, t->aux);                 /* set_sequence :287-290 */
+    } else {
+        h[0] = t->hdr0;                                     /* Gre::prepend_header + flag setters */
+        h[1] = t->hdr1;
+        put16(h + 2, t->inner_type);                        /* set_protocol_type */
+        const uint32_t cr = (h0 & 0xc0) ? 4 : 0;
+        if (cr) put16(h + 4, gre_fill ? 0 : t->aux);        /* set_checksum */
+        if (h0 & 0x20) put32(h + 4 + cr, t->id);            /* set_key */
+    }
+    if (!oracle_build_one(tmp, len, r, flags)) return 0;
+    if (gre_fill) put16(tmp + ts + 4, (uint16_t)~oracle_from_slice(tmp + ts, len - ts));
+    memcpy(f, tmp, len);
+    return 1;
+}
+
 static void span(uint64_t frames_bytes, const uint32_t* offsets, uint32_t stride,
                  uint32_t frame_len, uint32_t i, uint64_t* off, uint64_t* len) {
     if (offsets) {
@@ -310,5 +366,17 @@ void oracle_forward_batch(uint8_t* frames, uint64_t frames_bytes, const uint32_t
         keep[i] = (uint8_t)oracle_forward_one(frames + off, (uint32_t)len, &recs[i], dmac, smac,
                                               forbid, n_forbid,
                                               (fwd_flags & RPKT_F_IPV6) != 0);
+    }
+}
+
+void oracle_build_tunnel_batch(uint8_t* frames, uint64_t frames_bytes, const uint32_t* offsets,
+                               uint32_t stride, uint32_t frame_len, uint32_t n,
+                               const rpkt_rec_t* recs, const rpkt_tun_t* tun, uint32_t flags,
+                               uint8_t* built) {
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t off, len;
+        span(frames_bytes, offsets, stride, frame_len, i, &off, &len);
+        int b = oracle_build_tunnel_one(frames + off, (uint32_t)len, &recs[i], &tun[i], flags);
+        if (built) built[i] = (uint8_t)b;
     }
 }

@@ -260,13 +260,52 @@ __device__ __forceinline__ uint32_t chunk_end(Frame fr, uint32_t hdr_end) {
     return e < kWin - ph ? e : kWin - ph;
 }
 
+// The tunnel header rpkt_gpu_build_tunnel_batch writes (t: its first byte in the slot; tw
+// the rpkt_tun_t words; tail = the frame's bytes from the header on): the prepend_header
+// template + setters of Vxlan (vxlan/generated.rs:99-150: bytes 0-1 flags, group_id,
+// vni; byte 7 the template's 0), Gtpv1 (gtpv1/generated.rs:110-170: flags, message
+// type, length = remaining - 8, teid; a 12-B header's sequence, bytes 10-11 left as the
+// buffer holds them) or Gre (gre/generated.rs:95-230: flags, version, protocol_type; the
+// checksum word when C or R, 0 when the fill computes it; the key when K; offset and
+// sequence left as the buffer holds them).
+__device__ __forceinline__ uint32_t tun_hdr_len(uint32_t kind, uint32_t h0) {
+    return kind == RPKT_TUN_VXLAN ? 8u
+         : kind == RPKT_TUN_GTPU ? ((h0 & 7u) ? 12u : 8u)
+         : 4u + ((h0 & 0xc0u) ? 4u : 0u) + ((h0 & 0x20u) ? 4u : 0u) + ((h0 & 0x10u) ? 4u : 0u);
+}
+__device__ __forceinline__ void emit_tunnel(uint8_t* t, uint32_t kind, uint32_t tw1, uint32_t tw2,
+                                            uint32_t tw3, uint32_t tail, bool zero_ck) {
+    t[0] = (uint8_t)tw3;
+    t[1] = (uint8_t)(tw3 >> 8);
+    if (kind == RPKT_TUN_VXLAN) {
+        put_be16(t + 2, tw3 >> 16);                             // set_group_id
+        t[4] = (uint8_t)(tw2 >> 16);                            // set_vni
+        t[5] = (uint8_t)(tw2 >> 8);
+        t[6] = (uint8_t)tw2;
+        t[7] = 0u;
+    } else if (kind == RPKT_TUN_GTPU) {
+        put_be16(t + 2, tail - 8u);                             // set_packet_len(remaining)
+        put_be32(t + 4, tw2);                                   // set_teid
+        if (tw3 & 7u) put_be16(t + 8, tw3 >> 16);               // set_sequence
+    } else {
+        put_be16(t + 2, tw1 >> 16);                             // set_protocol_type
+        const uint32_t cr = (tw3 & 0xc0u) ? 4u : 0u;
+        if (cr) put_be16(t + 4, zero_ck ? 0u : tw3 >> 16);      // set_checksum
+        if (tw3 & 0x20u) put_be32(t + 4 + cr, tw2);             // set_key
+    }
+}
+
 // rpkt_gpu_build_batch: window -> headers composed in LDS -> checksums (IPv4 over the
 // slot; L4 over the slot plus the payload stream past the window) -> write-back.
-template <bool L4FILL>
+// TUN (rpkt_gpu_build_tunnel_batch): a tunnel header from tun[i] composed in the slot too,
+// before the sums (the outer UDP checksum covers it); a GRE checksum filled like an L4 one
+// with no pseudo header.
+template <bool L4FILL, bool TUN = false>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
 void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
                   uint32_t stride, uint32_t frame_len, uint32_t n,
-                  const rpkt_rec_t* __restrict__ recs, uint32_t flags, uint8_t* __restrict__ built) {
+                  const rpkt_rec_t* __restrict__ recs, uint32_t flags, uint8_t* __restrict__ built,
+                  const rpkt_tun_t* __restrict__ tun) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch[kWavesPerBlock];
     const int lane = threadIdx.x & (kWave - 1);
     const int wid = threadIdx.x / kWave;
@@ -309,19 +348,45 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
     const uint32_t fixed4 = proto == 17u ? 8u : (proto == 6u ? 20u : 0u);
     const bool fits = valid && nv <= RPKT_MAX_VLAN && !(proto == 6u && doff4 < 20u) &&
                       len >= l4 + l4hdr && !(proto == 17u && len - l4 > 65535u);
-    const bool ok = fits && (rec6 ? l4 >= l3 + 40u && len - l3 - 40u <= 65535u
-                                  : ihl4 >= 20u && len - l3 <= 65535u);
+    // the tunnel: VXLAN / GTP-U in the UDP payload (l4 + 8), GRE at l4 (protocol 47); the
+    // header must lie in the frame and in the LDS window, else the frame is not built
+    uint32_t tw1 = 0u, tw2 = 0u, tw3 = 0u, tkind = 0u, ts = 0u, thl = 0u;
+    bool tun_ok = true;
+    if constexpr (TUN) {
+        if (valid) {
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tun) + i);
+            tkind = t.x & 0xffu;
+            tw1 = t.y;
+            tw2 = t.z;
+            tw3 = t.w;
+        }
+        if (tkind != RPKT_TUN_NONE) {
+            ts = tkind == RPKT_TUN_GRE ? l4 : l4 + 8u;
+            thl = tun_hdr_len(tkind, tw3 & 0xffu);
+            tun_ok = tkind <= RPKT_TUN_GRE && proto == (tkind == RPKT_TUN_GRE ? 47u : 17u) &&
+                     len >= ts + thl && ts + thl <= RPKT_TUN_BUILD_MAX_END &&
+                     !(tkind == RPKT_TUN_GTPU && len - ts > 65543u);   // gtpv1/generated.rs:116
+        }
+    }
+    const bool ok = fits && tun_ok && (rec6 ? l4 >= l3 + 40u && len - l3 - 40u <= 65535u
+                                            : ihl4 >= 20u && len - l3 <= 65535u);
     // an IPv6 L4 header that does not lie whole in the window is written to global memory
     // by its lane (extension headers can push it past the window), never from the slot
     const bool far = ok && rec6 && fixed4 != 0u && ph + l4 + fixed4 > (uint32_t)kWin;
     const bool fill_ip = ok && !rec6 && (flags & RPKT_BUILD_IP_CSUM);
     const bool fill_l4 = L4FILL && ok && fixed4;
+    // the GRE checksum (checksum_present) with the L4 fill: RFC 2784 over the GRE header
+    // and payload, no pseudo header
+    const bool fill_gre = TUN && L4FILL && ok && tkind == RPKT_TUN_GRE && (tw3 & 0x80u);
     if (ok) {
-        emit_link(slot + ph, w, nv);
-        if (rec6) emit_ip6(slot + ph + l3, w, len - l3 - 40u);
-        else emit_ip4(slot + ph + l3, w, len - l3, fill_ip ? 0u : (w[8] >> 16));
+        if constexpr (TUN) {
+            if (tkind != RPKT_TUN_NONE) emit_tunnel(slot + ph + ts, tkind, tw1, tw2, tw3, len - ts, fill_gre);
+        }
         emit_l4(far ? frames + fr.off + l4 : slot + ph + l4, w, proto, len - l4,
                 fill_l4 ? 0u : (w[15] & 0xffffu));
+        if (rec6) emit_ip6(slot + ph + l3, w, len - l3 - 40u);
+        else emit_ip4(slot + ph + l3, w, len - l3, fill_ip ? 0u : (w[8] >> 16));
+        emit_link(slot + ph, w, nv);
     }
     if (fill_ip) {
         const uint32_t s = be_sum(lds_range_sum(slot, ph + l3, ph + l4), fr.off + l3);
@@ -334,7 +399,7 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         // info = fill | udp << 1 | far << 2 | l4 slot offset << 8
         uint32_t part = 0, ss = 0, se = 0, pseudo = 0;
         const uint32_t win_end = kWin - ph;
-        if (fill_l4) {
+        if (fill_l4 || fill_gre) {
             // the summed range starts at the L4 header, or past it (far: the header's
             // sum comes from the record's values); the in-window part, then the stream
             const uint32_t ps = far ? l4 + fixed4 : l4;
@@ -345,7 +410,9 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
                 ss = fr.off + s0;
                 se = fr.off + len;
             }
-            if (rec6) {                 // pseudo_v6: src, the final destination, length, nh
+            if (fill_gre) {
+                pseudo = 0u;            // GRE: the header and payload alone
+            } else if (rec6) {          // pseudo_v6: src, the final destination, length, nh
                 const FrameDw dw{slot, ph, fr.off, fb, rs};
                 uint32_t pd = w[8] >> 16;
                 if (pd < l3 + 24u || pd + 16u > l4) pd = l3 + 24u;   // as the oracle
@@ -355,10 +422,11 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
                 const uint32_t src = w[9], dst = w[10];
                 pseudo = (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu);
             }
-            pseudo += proto + (len - l4) + (far ? l4_hdr_sum(w, proto, len - l4) : 0u);
+            if (!fill_gre) pseudo += proto + (len - l4) + (far ? l4_hdr_sum(w, proto, len - l4) : 0u);
         }
-        *reinterpret_cast<uint32_t*>(slot + kWin) = (uint32_t)fill_l4 |
-            ((uint32_t)(proto == 17u) << 1) | ((uint32_t)far << 2) | ((ph + l4) << 8);
+        *reinterpret_cast<uint32_t*>(slot + kWin) = (uint32_t)(fill_l4 || fill_gre) |
+            ((uint32_t)(proto == 17u) << 1) | ((uint32_t)far << 2) | ((uint32_t)fill_gre << 3) |
+            ((ph + l4) << 8);
         uint32_t sp = 0;
         if constexpr (!kWholeFrame) sp = stream_rest<2>(X, rs, fb, ss, se, wend, fend, W, lane);
         const uint32_t info = *reinterpret_cast<const uint32_t*>(slot + kWin);
@@ -367,16 +435,18 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
             // (far: the summed range starts fixed4 bytes later, an even offset: same phase)
             const uint32_t sum = fold16(pseudo + be_sum(part + sp, (fr.off & ~15u) + at));
             uint32_t ck = ~sum & 0xffffu;
-            const bool udp = info & 2u;
-            if (ck == 0u && udp) ck = 0xffffu;                  // RFC 768 / RFC 8200 8.1
+            const bool udp = info & 2u, gre = info & 8u;
+            if (ck == 0u && udp && !gre) ck = 0xffffu;          // RFC 768 / RFC 8200 8.1
             uint8_t* t = (info & 4u) ? frames + (fr.off & ~15u) + at : slot + at;
-            put_be16(t + (udp ? 6u : 16u), ck);
+            put_be16(t + (gre ? 4u : (udp ? 6u : 16u)), ck);
         }
     }
     wave_sync();
     // the window holds the original bytes around the headers: round the written range
     // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
-    uint32_t r1 = ok ? line_end(fr, far ? l3 + 8u : l4 + fixed4) : 0u;
+    uint32_t hdr_end = far ? l3 + 8u : l4 + fixed4;
+    if (TUN && tkind != RPKT_TUN_NONE && ts + thl > hdr_end) hdr_end = ts + thl;
+    uint32_t r1 = ok ? line_end(fr, hdr_end) : 0u;
     r1 = far && r1 > l4 ? l4 : r1;                          // the L4 header went to memory
     write_back(rs, frames, W, lane, fr.off, r1);
     if (built && valid) built[i] = ok ? 1 : 0;
@@ -627,8 +697,34 @@ int RPKT_TX_FN(rpkt_gpu_build_batch)(const rpkt_batch_t* b, const rpkt_rec_t* re
     auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true> : build_kernel<false>;
     return launch(k, dim3(grid), dim3(per_block), kTxLdsPad, (hipStream_t)stream,
                   const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
-                  b->stride, flen, b->n, recs_dev, flags, built_dev);
+                  b->stride, flen, b->n, recs_dev, flags, built_dev,
+                  static_cast<const rpkt_tun_t*>(nullptr));
 }
+
+#ifndef RPKT_TX_W64
+// The encapsulation build (always the 128-B-window compile: a tunnel frame is longer than
+// a 64-B window).
+int rpkt_gpu_build_tunnel_batch(const rpkt_batch_t* b, const rpkt_rec_t* recs_dev,
+                                const rpkt_tun_t* tun_dev, uint32_t flags, uint8_t* built_dev,
+                                void* stream) {
+    if (!b || !recs_dev || !tun_dev) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_BUILD_IP_CSUM | RPKT_BUILD_L4_CSUM)) return RPKT_E_INVAL;
+    if (b->n == 0) return RPKT_OK;
+    if (!b->frames_dev) return RPKT_E_INVAL;
+    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)recs_dev & 15u) != 0 || ((uintptr_t)tun_dev & 15u) != 0 ||
+        ((uintptr_t)b->frames_dev & 15u) != 0)
+        return RPKT_E_ALIGN;
+    const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
+    const uint32_t per_block = kWave * kWavesPerBlock;
+    const uint32_t grid = (b->n + per_block - 1) / per_block;
+    auto k = (flags & RPKT_BUILD_L4_CSUM) ? build_kernel<true, true> : build_kernel<false, true>;
+    return launch(k, dim3(grid), dim3(per_block), kTxLdsPad, (hipStream_t)stream,
+                  const_cast<uint8_t*>(b->frames_dev), (uint32_t)b->frames_bytes, b->offsets_dev,
+                  b->stride, flen, b->n, recs_dev, flags, built_dev, tun_dev);
+}
+#endif
 
 int RPKT_TX_FN(rpkt_gpu_forward_batch)(const rpkt_batch_t* b, const rpkt_fwd_t* fwd,
                                        uint8_t* keep_dev, void* stream) {

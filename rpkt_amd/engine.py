@@ -60,7 +60,7 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
            "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact", "rpkt_gpu_coll_unique_id",
            "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy", "rpkt_gpu_comm_init_timeout",
-           "rpkt_gpu_comm_abort", "rpkt_gpu_parse_tunnel_batch"]
+           "rpkt_gpu_comm_abort", "rpkt_gpu_parse_tunnel_batch", "rpkt_gpu_build_tunnel_batch"]
 COLL_ID_BYTES = 128
 
 _lib = None
@@ -137,6 +137,10 @@ def lib():
                                                   ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_void_p]
         L.rpkt_gpu_parse_tunnel_batch.restype = ctypes.c_int
+        L.rpkt_gpu_build_tunnel_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.c_void_p, ctypes.c_void_p]
+        L.rpkt_gpu_build_tunnel_batch.restype = ctypes.c_int
         L.rpkt_gpu_layers_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.rpkt_gpu_layers_batch.restype = ctypes.c_int
@@ -502,6 +506,19 @@ def build_batch(batch, recs, flags=3, built=None, stream=None):
     rc = lib().rpkt_gpu_build_batch(ctypes.byref(d), recs.data_ptr(), flags, built.data_ptr(),
                                     _stream_ptr(stream))
     _check(rc, "rpkt_gpu_build_batch")
+    return built
+
+
+def build_tunnel_batch(batch, recs, tun, flags=3, built=None, stream=None):
+    """rpkt_gpu_build_tunnel_batch: the outer headers of recs plus each frame's tunnel
+    header of tun (uint8 tensors of n * 80 / n * 16 bytes); returns the built flags."""
+    torch = _torch()
+    if built is None:
+        built = torch.empty(batch.n, dtype=torch.uint8, device=batch.frames.device)
+    d = batch.desc()
+    rc = lib().rpkt_gpu_build_tunnel_batch(ctypes.byref(d), recs.data_ptr(), tun.data_ptr(),
+                                           flags, built.data_ptr(), _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_build_tunnel_batch")
     return built
 
 

@@ -439,6 +439,215 @@ class EtherFrame(_View):
         _put16(self.b, 12, value)
 
 
+# rpkt/src/vxlan/generated.rs:12, gtpv1/generated.rs (GTPV1_HEADER_TEMPLATE), gre/generated.rs
+VXLAN_HEADER_TEMPLATE = bytes(8)
+GTPV1_HEADER_TEMPLATE = bytes([0x30, 0xff, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00])   # :13
+GRE_HEADER_TEMPLATE = bytes(4)                                                    # :13
+
+
+class Vxlan(_View):
+    """vxlan/generated.rs:99-161: Vxlan::prepend_header + setters (the encapsulation build,
+    rpkt_gpu_build_tunnel_batch, vlan_mpls_tests.rs:254-300)."""
+    kind = 1
+
+    @classmethod
+    def prepend_header(cls, buf, header=VXLAN_HEADER_TEMPLATE):
+        assert len(header) == 8                              # :101 chunk_headroom >= 8
+        v = cls(buf, bytearray(header))
+        buf._push("vxlan", v, 8)
+        return v
+
+    def _bit(self, byte, bit, value):
+        self.b[byte] = (self.b[byte] & ~(1 << bit) & 0xff) | ((1 if value else 0) << bit)
+
+    def set_gbp_extention(self, v): self._bit(0, 7, v)          # :106
+    def set_vni_present(self, v): self._bit(0, 3, v)            # :116
+    def set_dont_learn(self, v): self._bit(1, 6, v)             # :129
+    def set_policy_applied(self, v): self._bit(1, 3, v)         # :139
+
+    def set_reserved_0(self, value):                           # :111
+        assert value <= 0x7
+        self.b[0] = (self.b[0] & 0x8f) | (value << 4)
+
+    def set_reserved_1(self, value):                           # :121
+        assert value <= 0xf
+        w = (value << 7) | ((self.b[0] & 0xf8) << 8) | (self.b[1] & 0x7f)
+        _put16(self.b, 0, w)
+
+    def set_reserved_2(self, value):                           # :134
+        assert value <= 0x3
+        self.b[1] = (self.b[1] & 0xcf) | (value << 4)
+
+    def set_reserved_3(self, value):                           # :144
+        assert value <= 0x7
+        self.b[1] = (self.b[1] & 0xf8) | value
+
+    def set_group_id(self, value):                             # :149
+        _put16(self.b, 2, value)
+
+    def set_vni(self, value):                                  # :153
+        assert value <= 0xffffff
+        self.b[4:7] = int(value).to_bytes(3, "big")
+
+    def set_reserved_4(self, value):                           # :158 (the build writes 0)
+        self.b[7] = value
+
+    def tun_fields(self):
+        assert self.b[7] == 0, "reserved_4: the build writes the template's 0"
+        return {"hdr0": self.b[0], "hdr1": self.b[1], "aux": _be16(self.b, 2),
+                "id": (self.b[4] << 16) | (self.b[5] << 8) | self.b[6]}, []
+
+
+class Gtpv1(_View):
+    """gtpv1/generated.rs:110-170, 254-310: Gtpv1::prepend_header(header) + setters
+    (gtpv1_test.rs:236-282); the extension headers after it are the caller's
+    (CursorMut.move_back with their bytes, as ExtPduNumber::prepend_header writes them)."""
+    kind = 2
+
+    @staticmethod
+    def header_len_of(header):
+        return 8 if (header[0] & 0x7) == 0 else 12          # :239-250
+
+    @classmethod
+    def prepend_header(cls, buf, header=GTPV1_HEADER_TEMPLATE):
+        assert len(header) == 8
+        hl = cls.header_len_of(header)
+        v = cls(buf, bytearray(header) + bytearray(hl - 8))
+        buf._push("gtpv1", v, hl)
+        assert buf.remaining() <= 65543                      # :116
+        _put16(v.b, 2, buf.remaining() - 8)                  # set_packet_len(remaining)
+        return v
+
+    @staticmethod
+    def set_header_flags(header, extention_header_present=None, sequence_present=None,
+                         npdu_present=None, message_type=None, teid=None):
+        """The setters on a header array (Gtpv1::from_header_array_mut, gtpv1_test.rs:249-256)."""
+        h = bytearray(header)
+        for bit, val in ((2, extention_header_present), (1, sequence_present), (0, npdu_present)):
+            if val is not None:
+                h[0] = (h[0] & ~(1 << bit) & 0xff) | ((1 if val else 0) << bit)
+        if message_type is not None:
+            h[1] = message_type
+        if teid is not None:
+            h[4:8] = int(teid).to_bytes(4, "big")
+        return bytes(h)
+
+    def header_len(self):
+        return self.header_len_of(self.b)
+
+    def set_teid(self, value):                                 # :163
+        self.b[4:8] = int(value).to_bytes(4, "big")
+
+    def set_message_type(self, value):                         # :159
+        self.b[1] = value
+
+    def set_sequence(self, value):                             # :287
+        assert self.header_len() == 12
+        _put16(self.b, 8, value)
+
+    def set_npdu(self, value):                                 # :297
+        assert self.header_len() == 12
+        self.b[10] = value
+
+    def set_next_extention_header(self, value):                # :307
+        assert self.header_len() == 12
+        self.b[11] = value
+
+    def tun_fields(self):
+        long = self.header_len() == 12
+        f = {"hdr0": self.b[0], "hdr1": self.b[1], "id": _be32(self.b, 4),
+             "aux": _be16(self.b, 8) if long else 0}
+        # npdu and next_extention_header are not in the record: the caller's bytes
+        return f, ([(10, bytes(self.b[10:12]))] if long else [])
+
+
+class Gre(_View):
+    """gre/generated.rs:104-340: Gre::prepend_header(header) + setters
+    (gre_test.rs:213-278); a GRE header follows an IPv4 / IPv6 header of protocol 47."""
+    kind = 3
+
+    @staticmethod
+    def header_len_of(header):                                 # gre/mod.rs:68-85
+        ind = _be16(header, 0)
+        return 4 + (4 if ind & 0xc000 else 0) + (4 if ind & 0x2000 else 0) + (4 if ind & 0x1000 else 0)
+
+    @classmethod
+    def prepend_header(cls, buf, header=GRE_HEADER_TEMPLATE):
+        assert len(header) == 4
+        hl = cls.header_len_of(header)
+        v = cls(buf, bytearray(header) + bytearray(hl - 4))
+        buf._push("gre", v, hl)
+        return v
+
+    def header_len(self):
+        return self.header_len_of(self.b)
+
+    @staticmethod
+    def set_header_flags(header, checksum_present=None, routing_present=None,
+                         key_present=None, sequence_present=None):
+        """The flag setters on a header array (Gre::from_header_array_mut + set_*_present,
+        :117-135, gre_test.rs:262-266): they decide the header's length."""
+        h = bytearray(header)
+        for bit, val in ((7, checksum_present), (6, routing_present), (5, key_present),
+                         (4, sequence_present)):
+            if val is not None:
+                h[0] = (h[0] & ~(1 << bit) & 0xff) | ((1 if val else 0) << bit)
+        return bytes(h)
+
+    def set_protocol_type(self, value):                        # :157
+        _put16(self.b, 2, value)
+
+    def set_checksum(self, value):                             # :297
+        assert self.b[0] & 0xc0
+        _put16(self.b, 4, value)
+
+    def set_offset(self, value):                               # :308
+        assert self.b[0] & 0xc0
+        _put16(self.b, 6, value)
+
+    def set_key(self, value):                                  # :318
+        assert self.b[0] & 0x20
+        at = 8 if self.b[0] & 0xc0 else 4
+        self.b[at:at + 4] = int(value).to_bytes(4, "big")
+
+    def set_sequence(self, value):                             # :332
+        assert self.b[0] & 0x10
+        at = 4 + (4 if self.b[0] & 0xc0 else 0) + (4 if self.b[0] & 0x20 else 0)
+        self.b[at:at + 4] = int(value).to_bytes(4, "big")
+
+    def tun_fields(self):
+        cr = 4 if self.b[0] & 0xc0 else 0
+        f = {"hdr0": self.b[0], "hdr1": self.b[1], "inner_type": _be16(self.b, 2),
+             "aux": _be16(self.b, 4) if cr else 0,
+             "id": _be32(self.b, 4 + cr) if self.b[0] & 0x20 else 0}
+        extra = [(6, bytes(self.b[6:8]))] if cr else []          # offset: the caller's
+        if self.b[0] & 0x10:                                      # sequence: the caller's
+            at = 4 + cr + (4 if self.b[0] & 0x20 else 0)
+            extra.append((at, bytes(self.b[at:at + 4])))
+        return f, extra
+
+
+def tunnel_record(buf):
+    """The rpkt_tun_t rpkt_gpu_build_tunnel_batch takes for a finished chain (kind NONE
+    without a tunnel view), and the frame bytes of the tunnel header the build leaves as
+    the buffer holds them (GTP npdu / next extension type, GRE offset / sequence)."""
+    from .records import TUN_DTYPE
+    t = np.zeros(1, dtype=TUN_DTYPE)[0]
+    base = buf.start
+    views = [(o, v) for k, o, v in buf.layers if k in ("vxlan", "gtpv1", "gre")]
+    assert len(views) <= 1, "one tunnel level"
+    extra = []
+    if views:
+        o, v = views[0]
+        fields, left = v.tun_fields()
+        t["kind"] = v.kind
+        t["tun_off"] = o - base
+        for k, x in fields.items():
+            t[k] = x
+        extra = [(o - base + at, b) for at, b in left]
+    return t, extra
+
+
 def assemble(records_extra, frame_lens, payloads=None):
     """A packed batch for rpkt_gpu_build_batch from finished chains: (frames buffer,
     u32 offsets, records).  Each frame is frame_len bytes: its payload (placed at the end)
