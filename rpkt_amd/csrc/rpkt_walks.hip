@@ -676,6 +676,129 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
     return stop;
 }
 
+// The straight-line prefix (RPKT_LAY_PREFIX): after the Ethernet step, the layers of the
+// common stack -- up to two VLAN tags, IPv4 or IPv6, TCP or UDP -- each as its own
+// specialised step (the walk_group + lay_next of those five groups, without the table:
+// VlanGroup vlan/generated.rs:312-322, Ipv4::parse ipv4/generated.rs:35-51, Ipv6::parse
+// ipv6/generated.rs:40-51, Udp::parse udp/generated.rs:31-42, Tcp::parse
+// tcp/generated.rs:34-45), stage by stage for the lanes whose walk is at such a layer; the
+// interpreter takes over at the first layer outside the set.  Same records as the
+// interpreter (tests/test_gpu_layers.py).
+#ifndef RPKT_LAY_PREFIX
+#define RPKT_LAY_PREFIX 0
+#endif
+__device__ __forceinline__ void lay_put(uint32_t (&o)[16], uint32_t nl, uint32_t p, uint32_t s) {
+    // layer nl <= 4 here: proto bytes in o[4..5], offsets in o[8..10]
+    const uint32_t pw = p << (8 * (nl & 3)), sw = s << (16 * (nl & 1));
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) o[4 + k] |= (nl >> 2) == k ? pw : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) o[8 + k] |= (nl >> 1) == k ? sw : 0u;
+}
+// the record's tail after a prefix layer (p) ended the step with (nx, key)
+__device__ __forceinline__ uint32_t lay_after(uint32_t (&o)[16], uint32_t nl, uint32_t p, int nx,
+                                              uint32_t key, uint32_t s, uint32_t e) {
+    const bool unk = nx == kNextUnknown;
+    const uint32_t stop = nx == kNextEnd ? (uint32_t)RPKT_L_END : unk ? (uint32_t)RPKT_L_UNKNOWN : 0u;
+    o[0] = nl | (stop << 8) | ((unk ? p : 0u) << 24);
+    o[1] = s & 0xffffu;
+    o[2] = e - s;
+    o[3] = unk ? key : 0u;
+    return stop;
+}
+__device__ __forceinline__ uint32_t lay_bad(uint32_t (&o)[16], uint32_t nl, uint32_t g, uint32_t s,
+                                            uint32_t e) {
+    o[0] = nl | ((uint32_t)RPKT_L_ERR << 8) | (g << 16);
+    o[1] = s & 0xffffu;
+    o[2] = e - s;
+    o[3] = 0u;
+    return RPKT_L_ERR;
+}
+// EtherType dispatch (lay_next's kNxEther without GRE's 0x6558)
+__device__ __forceinline__ int lay_by_et(const LayTable& T, uint32_t et) {
+    const uint32_t E = T.et[et_slot(et)];
+    return ((E >> 8) == et && et != 0x6558u) ? (int)(E & 0xffu) : kNextUnknown;
+}
+__device__ __forceinline__ void prefix_walk(LayerWin& Wn, LayHdr& H, const LayTable& T,
+                                            uint32_t (&o)[16], uint32_t& s, uint32_t& e,
+                                            uint32_t& nl, int& g, uint32_t& pend) {
+    // up to two VLAN tags
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        if (pend == 0u && g == RPKT_G_VLAN) {
+            const uint32_t r = e - s, et = be16_hi(H.F[0]);
+            const bool ef = et >= 0x0600u, d3 = et <= 1500u;
+            if ((r < 4u) | !(ef | d3) | (d3 & (et + 4u > r))) {
+                pend = lay_bad(o, nl, (uint32_t)g, s, e);
+            } else {
+                const uint32_t p = ef ? (uint32_t)RPKT_P_VLAN_VLANFRAME : (uint32_t)RPKT_P_VLAN_VLANDOT3FRAME;
+                lay_put(o, nl, p, s);
+                nl += 1u;
+                e = d3 ? s + 4u + et : e;
+                s += 4u;
+                const int nx = ef ? lay_by_et(T, et) : RPKT_G_LLC;
+                pend = lay_after(o, nl, p, nx, et, s, e);
+                g = nx;
+                H = lay_hdr(Wn, s, true);
+            }
+        }
+    }
+    // IPv4 / IPv6
+    if (pend == 0u && (g == RPKT_G_IPV4 || g == RPKT_G_IPV6)) {
+        const uint32_t r = e - s, F0 = H.F[0], F1 = H.F[1];
+        const bool v4 = g == RPKT_G_IPV4;
+        const uint32_t ihl = (F0 & 0xfu) * 4u, tot = be16_hi(F0), plen = be16_lo(F1);
+        const bool bad = v4 ? ((r < 20u) | (ihl < 20u) | (ihl > r) | (tot < ihl) | (tot > r))
+                            : ((r < 40u) | (plen + 40u > r));
+        if (bad) {
+            pend = lay_bad(o, nl, (uint32_t)g, s, e);
+        } else {
+            const uint32_t p = v4 ? (uint32_t)RPKT_P_IPV4_IPV4 : (uint32_t)RPKT_P_IPV6_IPV6;
+            lay_put(o, nl, p, s);
+            nl += 1u;
+            e = v4 ? s + tot : s + 40u + plen;
+            const uint32_t key = v4 ? (H.F[2] >> 8) & 0xffu : (F1 >> 16) & 0xffu;
+            const bool frag = v4 && (be16_hi(F1) & 0x1fffu) != 0u;   // a non-first fragment
+            s += v4 ? ihl : 40u;
+            const int nx = frag ? kNextEnd : (int)T.ip[key];
+            pend = lay_after(o, nl, p, nx, key, s, e);
+            g = nx;
+            H = lay_hdr(Wn, s, pend == 0u);
+        }
+    }
+    // TCP / UDP
+    if (pend == 0u && (g == RPKT_G_TCP || g == RPKT_G_UDP)) {
+        const uint32_t r = e - s, F0 = H.F[0];
+        const bool udp = g == RPKT_G_UDP;
+        const uint32_t ulen = be16_lo(H.F[1]), doff = ((H.F[3] >> 4) & 0xfu) * 4u;
+        const bool bad = udp ? ((r < 8u) | (ulen < 8u) | (ulen > r))
+                             : ((r < 20u) | (doff < 20u) | (doff > r));
+        if (bad) {
+            pend = lay_bad(o, nl, (uint32_t)g, s, e);
+        } else {
+            const uint32_t p = udp ? (uint32_t)RPKT_P_UDP_UDP : (uint32_t)RPKT_P_TCP_TCP;
+            lay_put(o, nl, p, s);
+            nl += 1u;
+            e = udp ? s + ulen : e;
+            s += udp ? 8u : doff;
+            // UDP: VXLAN / GTP-U / GTP-C by port, the GTP version from the payload's first
+            // byte (lay_next's kNxUdp); TCP ends the walk
+            const uint32_t dp = be16_hi(F0), sp = be16_lo(F0);
+            const bool dpt = (dp == 4789u) | (dp == 2152u) | (dp == 2123u);
+            const bool spt = (sp == 4789u) | (sp == 2152u) | (sp == 2123u);
+            const uint32_t port = udp ? (dpt ? dp : (spt ? sp : 0u)) : 0u;
+            const bool more = e > s;
+            const LayHdr H2 = lay_hdr(Wn, s, port != 0u && (port == 4789u || more));
+            const uint32_t gv = (H2.F[0] & 0xffu) >> 5;
+            const int gtp = gv == 1u ? RPKT_G_GTPV1 : (gv == 2u ? RPKT_G_GTPV2 : kNextUnknown);
+            const int nx = !port ? kNextEnd : (port == 4789u ? RPKT_G_VXLAN : (more ? gtp : kNextEnd));
+            pend = lay_after(o, nl, p, nx, gv, s, e);
+            g = nx;
+            H = H2;
+        }
+    }
+}
+
 // Lane L of a wave walks frames base + L + 64 k, k = 0 .. F-1, one after the other: a
 // walk's depth varies from frame to frame (the capture mix: 2.6 layers on average, a
 // wave's deepest lane 6.8), and a wave runs until its deepest lane ends, so a lane
@@ -782,7 +905,10 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
     constexpr bool kEth = DYN && RPKT_LAY_ETHER_FIRST;
     uint32_t pend = 0;
     if constexpr (kEth) {
-        if (active) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
+        if (active) {
+            pend = ether_step(Wn, H, T, e, o, s, e, nl, g);   // H: the header at 14, in the slot
+            if constexpr (RPKT_LAY_PREFIX) prefix_walk(Wn, H, T, o, s, e, nl, g, pend);
+        }
         if constexpr ((ABL & 4) != 0) pend = active ? (uint32_t)RPKT_L_END : 0u;
     }
     while (__ballot(active)) {
@@ -966,8 +1092,12 @@ void layers_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     } else {
                         Wn.refill(0u);
                     }
-                    if constexpr (kEth) pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
-                    else H = lay_hdr(Wn, 0u, false);
+                    if constexpr (kEth) {
+                        pend = ether_step(Wn, H, T, e, o, s, e, nl, g);
+                        if constexpr (RPKT_LAY_PREFIX) prefix_walk(Wn, H, T, o, s, e, nl, g, pend);
+                    } else {
+                        H = lay_hdr(Wn, 0u, false);
+                    }
                     if constexpr ((ABL & 4) != 0) pend = (uint32_t)RPKT_L_END;
                 }
             }

@@ -37,7 +37,7 @@ def test_chain_fuzz_parity(torch, flags):
     g = gpu_chain_records(hc.buf, hc.segs, hc.chain_first, flags)
     o = oracle.parse_chains(hc.buf, hc.segs, hc.chain_first, flags)
     assert_same(g, o)
-    assert len(set(o["status"].tolist())) == 14
+    assert len(set(o["status"].tolist())) == 15
 
 
 def test_chain_fuzz_flow_events(torch):
