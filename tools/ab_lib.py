@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7|ring2|ringc2]
+Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7|ring2|ringc2|tunnel13]
 (ring<cfg> / ringc<cfg>: the R rotated batches as one rpkt_gpu_parse_ring[_compact] launch)
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
@@ -112,6 +112,17 @@ def main():
             outs[name + "_recs"] = rec
             call[name] = (lambda k, fn=fn, out=out, rec=rec: fn(
                 ctypes.byref(descs[k % R]), 3, rec.data_ptr(), out.data_ptr(), None, 0, sp))
+        elif mode == "tunnel":                      # rpkt_gpu_parse_tunnel_batch, all sums
+            fn = L.rpkt_gpu_parse_tunnel_batch
+            fn.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                           ctypes.c_void_p]
+            rec = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
+            tun = torch.zeros(hb.n * 16, dtype=torch.uint8, device="cuda")
+            out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
+            outs[name + "_outer"], outs[name + "_tun"] = rec, tun
+            flags = args.flags if args.flags is not None else gen.FLAGS.get(cfg, 3)
+            call[name] = (lambda k, fn=fn, out=out, rec=rec, tun=tun, flags=flags: fn(
+                ctypes.byref(descs[k % R]), flags, rec.data_ptr(), tun.data_ptr(), out.data_ptr(), sp))
         elif mode == "layers":
             L.rpkt_gpu_layers_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p]
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")
