@@ -683,9 +683,12 @@ __device__ __forceinline__ uint32_t ether_step(LayerWin& Wn, LayHdr& H, const La
 // ipv6/generated.rs:40-51, Udp::parse udp/generated.rs:31-42, Tcp::parse
 // tcp/generated.rs:34-45), stage by stage for the lanes whose walk is at such a layer; the
 // interpreter takes over at the first layer outside the set.  Same records as the
-// interpreter (tests/test_gpu_layers.py).
+// interpreter (tests/test_gpu_layers.py).  Same process, byte-identical (round 6,
+// profiles/r06_lay_prefix/): config 5's walk 304.4 -> 262.2 us, config 2 42.9 -> 37.2 us,
+// the capture mix 57.2 -> 57.3 us (its VALU per wave 5375 -> 5585: the many stacks that
+// leave the prefix early pay its stages on top of the interpreter's).
 #ifndef RPKT_LAY_PREFIX
-#define RPKT_LAY_PREFIX 0
+#define RPKT_LAY_PREFIX 1        // 0: the interpreter from the first layer after Ethernet
 #endif
 __device__ __forceinline__ void lay_put(uint32_t (&o)[16], uint32_t nl, uint32_t p, uint32_t s) {
     // layer nl <= 4 here: proto bytes in o[4..5], offsets in o[8..10]
