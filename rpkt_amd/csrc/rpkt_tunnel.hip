@@ -3,17 +3,20 @@
 // every sum of both levels, in one pass per 64-frame tile (include/rpkt_gpu.h documents
 // the records and the dispatch; oracle/rpkt_oracle_tunnel.c restates it on the CPU).
 //
-// One wavefront per tile, as parse_kernel: the outer header windows go to LDS and each
+// One wavefront per tile, as parse_kernel: the outer header windows go to LDS (on long
+// tiles together with each frame's tail line, whose sum is taken there and then) and each
 // lane runs parse_lane on its frame; the lane then decodes the tunnel header(s) from the
 // same window (FrameDw: global memory past it), the outer record is staged in a second
-// LDS area, the inner frames' header windows replace the outer ones (their lines were just
-// fetched: mostly L2 hits) and parse_lane runs again from the inner frame's first byte
-// (its IP header for GTP-U and GRE).  The L4 bytes past the inner windows are summed by
-// one flattened chunk stream (rpkt_common.h); the outer L4 sum (UDP, or GRE with its
-// checksum), whose range contains the inner one, takes the inner stream's sum for the
-// bytes they share and streams only the rest -- the bytes between the outer window and
-// the inner stream (inside the inner window's lines) and any trailer after the inner
-// packet -- so each payload byte leaves HBM about once for all four sums.
+// LDS area, and the inner frame's window is made from the outer one: the chunks they
+// share move down the lane's slot and only the chunks past the outer window are loaded.
+// parse_lane runs again from the inner frame's first byte (its IP header for GTP-U and
+// GRE).  One flattened chunk stream (rpkt_common.h) then sums each lane's main range --
+// the inner L4 bytes past the inner window, or the outer L4 range without a tunnel -- and
+// the outer L4 sum (UDP, or GRE with its checksum), whose range contains the inner one,
+// is composed from the outer window's part, the inner window's part (LDS), the main
+// stream's sum when the rest of the two ranges is the same, and a rare stream for bytes
+// before the inner window or a trailer after the inner packet.  Each payload byte leaves
+// HBM about once for all four sums (PMC reads 1.04x the frame bytes on config 13).
 #include "rpkt_common.h"
 
 namespace {
@@ -185,6 +188,116 @@ __device__ __forceinline__ void flush_stage(const uint32_t* rl, int lane, rpkt_r
     }
 }
 
+// Absolute-phase word sum of LDS slot bytes [s, e) (slot byte 0 on a 16-B boundary).
+__device__ __forceinline__ uint32_t slot_range_sum(const uint8_t* slot, uint32_t s, uint32_t e) {
+    if (e <= s) return 0u;
+    uint32_t acc = 0;
+    uint32_t a = s & ~3u;
+    for (; a + 12u < e; a += 16u) {
+        const uint32_t x0 = lds32(slot, a), x1 = lds32(slot, a + 4u);
+        const uint32_t x2 = lds32(slot, a + 8u), x3 = lds32(slot, a + 12u);
+        acc = hsum(x3, hsum(x2, hsum(x1, hsum(x0, acc))));
+    }
+    for (; a < e; a += 4) acc = hsum(lds32(slot, a), acc);
+    acc -= halves(low_bytes(lds32(slot, s & ~3u), s & 3u));
+    if (e & 3u) acc -= halves(lds32(slot, e & ~3u) & ~((1u << (8u * (e & 3u))) - 1u));
+    return acc;
+}
+
+// The outer header windows, and with them (joint) each frame's tail line [tb, fend): the
+// line the next frame's window starts in, fetched in the same load group as that window
+// (the cooperative mapping of window_with_edges: chunk k of lane l is piece l % 8 of frame
+// 8 k + l / 8), so the stream never fetches it a second time.  Returns this lane's tail sum.
+__device__ __forceinline__ uint32_t outer_window_tail(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                      WaveScratch& W, int lane, Frame fr,
+                                                      uint32_t tb, uint32_t fend) {
+    const int j = lane & 7;
+    constexpr int kHalf = kWinChunks / 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u32x4 dw[kHalf], dt[kHalf];
+        uint32_t aw[kHalf], at[kHalf], lt[kHalf];
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            const int k = h * kHalf + i;
+            const int q = (k * kWave + lane) >> 3;
+            const uint32_t qo = (uint32_t)__shfl((int)fr.off, q, kWave);
+            const uint32_t qn = (uint32_t)__shfl((int)fr.len, q, kWave);
+            const uint32_t qt = (uint32_t)__shfl((int)tb, q, kWave);
+            const uint32_t qe = (uint32_t)__shfl((int)fend, q, kWave);
+            const uint32_t a = (qo & ~15u) + 16u * j, y = qt + 16u * j;
+            aw[i] = a < qo + qn ? a : fb;
+            const bool tin = y < qe;
+            at[i] = tin ? y : fb;
+            lt[i] = tin ? (qe - y < 16u ? qe - y : 16u) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            dw[i] = load16_fast<0>(rs, aw[i]);
+            dt[i] = load16_fast<0>(rs, at[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+            const int k = h * kHalf + i;
+            u32x4 v = dw[i], vt = dt[i];
+            if (__builtin_expect(straddles(aw[i], fb), 0)) v = load16(rs, aw[i], fb);
+            if (__builtin_expect(lt[i] != 0 && straddles(at[i], fb), 0)) vt = load16(rs, at[i], fb);
+            put_chunk(W, k * kWave + lane, v);
+            const uint32_t xt = sum8_lanes(lt[i] ? chunk_sum(vt, 0, (int)lt[i]) : 0u);
+            if (j == 0) W.last[(k * kWave + lane) >> 3] = xt;
+        }
+    }
+    wave_sync();
+    return W.last[lane];
+}
+
+// The inner window from the outer one: a lane whose inner frame starts d chunks into its
+// outer window moves chunks d.. of its slot down to 0.. (its own slot: no other lane reads
+// it), then the wave loads only the chunks past the outer window (cooperatively, the
+// window_issue mapping) and writes them into the slots.  Lanes without a tunnel keep
+// their outer window.
+__device__ __forceinline__ void inner_window_reuse(__amdgpu_buffer_rsrc_t rs, uint32_t fb,
+                                                   WaveScratch& W, int lane, uint32_t a1,
+                                                   uint32_t keep, uint32_t lim) {
+    u32x4 d[kWinChunks];
+    uint32_t addr[kWinChunks];
+    uint32_t fix = 0;
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) {
+        const int c = k * kWave + lane;
+        const int q = c / kWinChunks, j = c % kWinChunks;
+        const uint32_t qa = (uint32_t)__shfl((int)a1, q, kWave);
+        const uint32_t qk = (uint32_t)__shfl((int)keep, q, kWave);
+        const uint32_t ql = (uint32_t)__shfl((int)lim, q, kWave);
+        const uint32_t a = qa + 16u * j;
+        addr[k] = ((uint32_t)j >= qk && a < ql) ? a : fb;
+        fix |= (uint32_t)straddles(addr[k], fb) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) d[k] = load16_fast<0>(rs, addr[k]);
+    const uint32_t sh = (uint32_t)kWinChunks - keep;              // chunks moved down
+    if (keep != (uint32_t)kWinChunks && keep != 0u) {
+        uint32_t* sl = reinterpret_cast<uint32_t*>(&W.win[lane * kSlot]);
+        for (uint32_t j = 0; j < keep; ++j) {
+            const uint32_t x0 = sl[4 * (j + sh)], x1 = sl[4 * (j + sh) + 1];
+            const uint32_t x2 = sl[4 * (j + sh) + 2], x3 = sl[4 * (j + sh) + 3];
+            sl[4 * j] = x0;
+            sl[4 * j + 1] = x1;
+            sl[4 * j + 2] = x2;
+            sl[4 * j + 3] = x3;
+        }
+    }
+    wave_sync();                                      // every slot moved before the writes
+#pragma unroll
+    for (int k = 0; k < kWinChunks; ++k) {
+        if (addr[k] == fb) continue;
+        u32x4 v = d[k];
+        if (__builtin_expect(fix & (1u << k), 0)) v = load16(rs, addr[k], fb);
+        put_chunk(W, k * kWave + lane, v);
+    }
+    wave_sync();
+}
+
 template <bool L4>
 __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
                                             const uint8_t* __restrict__ frames, uint32_t fb,
@@ -199,15 +312,26 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
     // header-only batches read each line once: non-temporal window loads (as parse_tile)
     constexpr int kWinAux = L4 ? 0 : 2;
 
-    // 1. the outer header windows -> LDS, the outer parse
+    // 1. the outer header windows -> LDS (with the frames' tail lines on long tiles), the
+    // outer parse
     const Frame fr = spans.get(i);
-    {
+    const uint32_t a0 = fr.off & ~15u, fend = fr.off + (valid ? fr.len : 0u);
+    [[maybe_unused]] uint32_t tb = fend, tail_sum = 0u;
+    bool joint = false;
+    if constexpr (L4) {
+        const uint32_t wend0 = a0 + kWin;
+        if (fend > wend0) tb = max(fend & ~127u, wend0);
+        joint = wave_sum(fend > wend0 ? fend - wend0 : 0u) > kEdgeWindowBytes;   // uniform
+    }
+    if (joint) {
+        tail_sum = outer_window_tail(rs, fb, W, lane, fr, tb, fend);
+    } else {
         u32x4 d[kWinChunks];
         uint32_t addr[kWinChunks];
         const uint32_t fix = window_issue<kWinAux>(rs, fb, fr, lane, d, addr);
         window_commit(W, rs, fb, d, addr, fix, lane);
+        wave_sync();
     }
-    wave_sync();
     LaneRec L;
     parse_lane(W, lane, fr, valid, flags, L, rs, fb);
 
@@ -224,14 +348,12 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
 
     // 4. the inner header windows -> LDS (the outer ones are no longer read), inner parse
     const Frame fi = T.ok ? Frame{fr.off + T.is, T.ie - T.is} : Frame{0u, 0u};
-    {
-        u32x4 d[kWinChunks];
-        uint32_t addr[kWinChunks];
-        const uint32_t fix = window_issue<kWinAux>(rs, fb, fi, lane, d, addr);
-        wave_sync();                                  // every lane done with its outer window
-        window_commit(W, rs, fb, d, addr, fix, lane);
-    }
-    wave_sync();
+    const uint32_t a1 = T.ok ? fi.off & ~15u : a0;
+    const uint32_t dch = (a1 - a0) >> 4;
+    const uint32_t keep = dch < (uint32_t)kWinChunks ? (uint32_t)kWinChunks - dch : 0u;
+    // (chunks loaded up to the outer frame's end: the outer L4 range's part in this window
+    // is summed from it below, and it can run past the inner frame)
+    inner_window_reuse(rs, fb, W, lane, a1, T.ok ? keep : (uint32_t)kWinChunks, fend);
     parse_lane(W, lane, fi, T.ok, flags, L, rs, fb, T.start_et, T.is);
     if (!T.ok) {
 #pragma unroll
@@ -240,19 +362,39 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
         L.want_l4 = false;
         L.stream_s = L.stream_e = 0u;
     }
+    // the outer L4 range's bytes the inner window holds: [max(o_ss, a1), min(o_se, a1 + 128))
+    [[maybe_unused]] uint32_t o_lds = 0u;
+    if constexpr (L4) {
+        if (T.ok && o_want) {
+            const uint32_t ls = o_ss > a1 ? o_ss : a1, le = o_se < a1 + kWin ? o_se : a1 + kWin;
+            o_lds = slot_range_sum(&W.win[lane * kSlot], ls - a1, le > ls ? le - a1 : ls - a1);
+        }
+    }
     stage_record(W, lane, L.w);
 
     // 5. L4 bytes past the windows: the inner stream, then the outer range's other bytes
     if constexpr (L4) {
-        const uint32_t sp_i = wave_stream_sum<2>(rs, fb, L.stream_s, L.stream_e, W, lane);
-        const bool shared = o_want && L.want_l4 && L.stream_e > L.stream_s &&
-                            L.stream_s >= o_ss && L.stream_e <= o_se;
-        const uint32_t x = shared ? L.stream_s : o_se, y = shared ? L.stream_e : o_se;
-        uint32_t sp_o = wave_stream_sum<2>(rs, fb, o_want ? o_ss : 0u, o_want ? x : 0u, W, lane);
-        sp_o += wave_stream_sum<2>(rs, fb, o_want ? y : 0u, o_want ? o_se : 0u, W, lane);
-        if (shared) sp_o += sp_i;
+        // one main stream per lane: the inner L4 range (the outer one without a tunnel),
+        // less the tail line summed with the windows when the range runs to the frame end
+        const uint32_t ms = T.ok ? L.stream_s : (o_want ? o_ss : 0u);
+        const uint32_t me = T.ok ? L.stream_e : (o_want ? o_se : 0u);
+        const bool use_tail = joint && me > ms && me == fend && tb < fend && tb >= ms;
+        const uint32_t sp_m = wave_stream_sum<2>(rs, fb, ms, use_tail ? tb : me, W, lane) +
+                              (use_tail ? tail_sum : 0u);
+        // the outer range of a tunnel frame: [o_ss, a1) streamed (an inner window past the
+        // outer one), the inner window's part from LDS, [a1 + 128, o_se) the main stream when
+        // it is the same range, else streamed
+        const uint32_t w1 = a1 + kWin;
+        const uint32_t p3s = o_ss > w1 ? o_ss : w1;
+        const bool shared = T.ok && o_want && p3s == ms && o_se == me && me > ms;
+        const bool rest = T.ok && o_want;
+        uint32_t sp_o = wave_stream_sum<2>(rs, fb, rest ? o_ss : 0u,
+                                           rest ? (o_se < a1 ? o_se : a1) : 0u, W, lane);
+        sp_o += wave_stream_sum<2>(rs, fb, rest && !shared ? p3s : 0u,
+                                   rest && !shared ? o_se : 0u, W, lane);
+        sp_o += T.ok ? o_lds + (shared ? sp_m : 0u) : sp_m;
         if (L.want_l4)
-            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + be_sum(L.l4_part + sp_i, L.l4_start_abs)) << 16;
+            rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + be_sum(L.l4_part + sp_m, L.l4_start_abs)) << 16;
         if (o_want) OS[lane * 21 + 18] |= fold16(o_pseudo + be_sum(o_part + sp_o, o_abs)) << 16;
     }
 

@@ -6,7 +6,7 @@ set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
 RND=${RND:-r02}
-for t in ${TAGS:-c2 c3 c4 c5 c7 c10 c11 c2_compact c3_compact c11_compact c5_opts c5_opts_compact walks build3 optsc5 build11 forward10 opts11}; do
+for t in ${TAGS:-c2 c3 c4 c5 c7 c10 c11 c2_compact c3_compact c11_compact c5_opts c5_opts_compact walks build3 optsc5 build11 forward10 opts11 tunnel13 encap13}; do
     P=$G/prof_$t; D=$R/profiles/${RND}_$t
     mkdir -p "$D"
     cp "$P/trace_kernel_stats.csv" "$P/trace_bench.log" "$D/"
@@ -16,7 +16,7 @@ for t in ${TAGS:-c2 c3 c4 c5 c7 c10 c11 c2_compact c3_compact c11_compact c5_opt
         python3 "$R/tools/pmc_by_kernel.py" "$P/${k}_counter_collection.csv" > "$D/${k}_by_kernel.json"
     done
     if [ "$t" = build3 ] || [ "$t" = optsc5 ] || [ "$t" = build11 ] || [ "$t" = forward10 ] ||
-       [ "$t" = opts11 ]; then
+       [ "$t" = opts11 ] || [ "$t" = tunnel13 ] || [ "$t" = encap13 ]; then
         python3 "$R/tools/traffic.py" "$P" tx:$t "$R/profiles/traffic_tx.json"
     elif [ "$t" = walks ]; then
         python3 "$R/tools/traffic.py" "$P" tx "$R/profiles/traffic_tx.json"

@@ -91,7 +91,7 @@ TX_LEGS = {"build2": "build_kernel", "forward2": "forward_kernel", "opts5": "opt
 
 
 LEG_UNIT = {"build": "tx", "forward": "tx", "opts": "walks", "optsc": "walks", "layers": "walks",
-            "fields": "fields"}
+            "fields": "fields", "tunnel": "tunnel", "encap": "tx"}
 
 
 def unit_hash(build, unit):
@@ -104,7 +104,8 @@ def unit_hash(build, unit):
 
 MODE_KERNEL = {"build": "build_kernel", "forward": "forward_kernel", "opts": "options_kernel",
                "optsc": "options_kernel",
-               "layers": "layers_kernel", "fields": "fields_kernel"}
+               "layers": "layers_kernel", "fields": "fields_kernel", "tunnel": "tunnel_kernel",
+               "encap": "build_kernel"}
 
 
 def main_tx(prof, out, only=None):
@@ -126,8 +127,13 @@ def main_tx(prof, out, only=None):
         with open(out) as fh:
             old = json.load(fh)
     if only:
-        assert old.get("engine_build") == build, (old.get("engine_build"), build)
-        legs = old["legs"]
+        # a single-leg profile joins the summary of its kernel unit's current source
+        unit = LEG_UNIT[only.rstrip("0123456789")]
+        assert old.get("engine_build") == build or \
+            unit_hash(old.get("engine_build"), unit) == unit_hash(build, unit) or \
+            unit_hash(old.get("engine_build"), unit) is None, (old.get("engine_build"), build)
+        legs = {k: dict(v, engine_build=v.get("engine_build", old.get("engine_build")))
+                for k, v in old["legs"].items()}
     else:
         # the single-leg profiles (build3, optsc5) stay while their kernel unit's source
         # is unchanged; each leg carries the build it was measured on
