@@ -252,13 +252,18 @@ struct Ip6Hdr {
     uint64_t trace;
     bool mal, has_ra, has_g;
 };
+// RPKT_IP6_STEP2: a step takes a Pad0 run and the option after it (as the IPv4 / TCP
+// walks' step does), instead of one step each.
+#ifndef RPKT_IP6_STEP2
+#define RPKT_IP6_STEP2 1
+#endif
 __device__ __forceinline__ Ip6Hdr ip6_hdr_walk(const OptDw& dw, uint32_t c, uint32_t hl) {
     Ip6Hdr R{0u, 0u, 0u, 0u, 0u, 0u, 0ull, false, false, false};
     const uint32_t s0 = c + 2u, nb = hl - 2u;
     uint32_t pos = 0;
     while (pos < nb) {
-        const uint32_t d = dw(s0 + pos);
-        const uint32_t t = d & 0xffu, rem = nb - pos;
+        uint32_t d = dw(s0 + pos);
+        uint32_t t = d & 0xffu, rem = nb - pos;
         if (t == 0u) {                                  // a run of Pad0 (up to 4 bytes)
             uint32_t kz = d ? (uint32_t)__builtin_ctz(d) >> 3 : 4u;
             kz = kz < rem ? kz : rem;
@@ -267,7 +272,11 @@ __device__ __forceinline__ Ip6Hdr ip6_hdr_walk(const OptDw& dw, uint32_t c, uint
                                    : 0ull;
             R.cnt += kz;
             pos += kz;
-            continue;
+            // a run shorter than 4 that the header does not cut ends at an option
+            if (!RPKT_IP6_STEP2 || kz == 4u || pos >= nb) continue;
+            d = dw(s0 + pos);
+            t = d & 0xffu;
+            rem = nb - pos;
         }
         const uint32_t ln = ((d >> 8) & 0xffu) + 2u;                     // header_len
         const bool ok = t == 5u ? (rem >= 4u && ln == 4u) : (rem >= 2u && ln <= rem);
