@@ -298,6 +298,13 @@ __device__ __forceinline__ void inner_window_reuse(__amdgpu_buffer_rsrc_t rs, ui
     wave_sync();
 }
 
+// chunk loads in flight per lane in the main stream: the second record stage holds the
+// kernel at 10 waves per CU (the parse runs 16), so each wave keeps more loads in flight
+#ifndef RPKT_TUN_UNROLL
+#define RPKT_TUN_UNROLL 4
+#endif
+constexpr int kTunUnroll = RPKT_TUN_UNROLL;
+
 template <bool L4>
 __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
                                             const uint8_t* __restrict__ frames, uint32_t fb,
@@ -379,7 +386,7 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
         const uint32_t ms = T.ok ? L.stream_s : (o_want ? o_ss : 0u);
         const uint32_t me = T.ok ? L.stream_e : (o_want ? o_se : 0u);
         const bool use_tail = joint && me > ms && me == fend && tb < fend && tb >= ms;
-        const uint32_t sp_m = wave_stream_sum<2>(rs, fb, ms, use_tail ? tb : me, W, lane) +
+        const uint32_t sp_m = wave_stream_sum<2, kTunUnroll>(rs, fb, ms, use_tail ? tb : me, W, lane) +
                               (use_tail ? tail_sum : 0u);
         // the outer range of a tunnel frame: [o_ss, a1) streamed (an inner window past the
         // outer one), the inner window's part from LDS, [a1 + 128, o_se) the main stream when
