@@ -2,7 +2,7 @@
 every leg's full result) and the committed PMC traffic summaries
 (profiles/traffic_*.json).  Host side.
 
-Usage: python tools/design_table.py profiles/r05_bench_detail.json [--print]
+Usage: python tools/design_table.py profiles/r06_bench_final_detail.json [--print]
 """
 import json
 import os
@@ -46,6 +46,10 @@ ROWS = [
     ("options 5 standalone (80-B / 16-B records)", ("tx_opts5", "tx_optsc5"), "traffic_tx",
      ("opts5", "optsc5")),
     ("options 11 standalone (TCP + `Ipv6OptionsIter`)", "tx_opts11", "traffic_tx", "opts11"),
+    ("**tunnel 13**: 1M × 1500 B VXLAN / GTP-U / GRE, outer + inner, all sums", "tx_tunnel13",
+     "traffic_tx", "tunnel13"),
+    ("encapsulation 13 (VXLAN / GTP-U / GRE headers + outer, checksums filled)", "tx_encap13",
+     "traffic_tx", "encap13"),
     ("layers 9 (capture mix)", "tx_layers9", "traffic_tx", "layers9"),
     ("fields 9 (16 getters)", "tx_fields9", "traffic_tx", "fields9"),
 ]
