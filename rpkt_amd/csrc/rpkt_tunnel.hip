@@ -6,8 +6,10 @@
 // One wavefront per tile, as parse_kernel: the outer header windows go to LDS (on long
 // tiles together with each frame's tail line, whose sum is taken there and then) and each
 // lane runs parse_lane on its frame; the lane then decodes the tunnel header(s) from the
-// same window (FrameDw: global memory past it), the outer record is staged in a second
-// LDS area, and the inner frame's window is made from the outer one: the chunks they
+// same window (FrameDw: global memory past it), the outer record waits in registers (its
+// words 0..11 in LDS past the inner record's stage once that is written: 128 VGPRs and
+// 9.7 KB of LDS per wave, 16 waves per CU), and the inner frame's window is made from the
+// outer one: the chunks they
 // share move down the lane's slot and only the chunks past the outer window are loaded.
 // parse_lane runs again from the inner frame's first byte (its IP header for GTP-U and
 // GRE).  One flattened chunk stream (rpkt_common.h) then sums each lane's main range --
@@ -298,15 +300,15 @@ __device__ __forceinline__ void inner_window_reuse(__amdgpu_buffer_rsrc_t rs, ui
     wave_sync();
 }
 
-// chunk loads in flight per lane in the main stream: the second record stage holds the
-// kernel at 10 waves per CU (the parse runs 16), so each wave keeps more loads in flight
+// chunk loads in flight per lane in the main stream (6 and 8 measured: no gain, and 8 costs
+// occupancy)
 #ifndef RPKT_TUN_UNROLL
 #define RPKT_TUN_UNROLL 4
 #endif
 constexpr int kTunUnroll = RPKT_TUN_UNROLL;
 
 template <bool L4>
-__device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
+__device__ __forceinline__ void tunnel_tile(WaveScratch& W,
                                             const uint8_t* __restrict__ frames, uint32_t fb,
                                             const uint32_t* __restrict__ offsets, uint32_t stride,
                                             uint32_t frame_len, uint32_t n, uint32_t flags,
@@ -346,9 +348,11 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
     const Tunnel T = decode_tunnel(L, FrameDw{&W.win[lane * kSlot], fr.off & 15u, fr.off, fb, rs},
                                    flags);
 
-    // 3. the outer record to its own stage; its L4 sum state kept for the streams
+    // 3. the outer record in registers through the inner parse (a second LDS stage for it
+    // held the kernel at 10 waves per CU), its L4 sum state kept for the streams
+    uint32_t ow[20];
 #pragma unroll
-    for (int k = 0; k < 20; ++k) OS[lane * 21 + k] = L.w[k];
+    for (int k = 0; k < 20; ++k) ow[k] = L.w[k];
     [[maybe_unused]] const uint32_t o_ss = L.stream_s, o_se = L.stream_e, o_part = L.l4_part;
     [[maybe_unused]] const uint32_t o_abs = L.l4_start_abs, o_pseudo = L.pseudo;
     [[maybe_unused]] const bool o_want = L.want_l4;
@@ -378,6 +382,12 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
         }
     }
     stage_record(W, lane, L.w);
+    // the outer record's words 0..11 wait in the window area past the inner stage (free
+    // now: 3072 B, word-major), so the streams hold 8 of its words in registers, not 20
+    static_assert(kWave * 21 * 4 + 12 * kWave * 4 <= kWinArea, "parked words fit past the stage");
+    uint32_t* park = reinterpret_cast<uint32_t*>(&W.win[kWave * 21 * 4]);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) park[k * kWave + lane] = ow[k];
 
     // 5. L4 bytes past the windows: the inner stream, then the outer range's other bytes
     if constexpr (L4) {
@@ -402,18 +412,21 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W, uint32_t* OS,
         sp_o += T.ok ? o_lds + (shared ? sp_m : 0u) : sp_m;
         if (L.want_l4)
             rec_stage(W)[lane * 21 + 18] |= fold16(L.pseudo + be_sum(L.l4_part + sp_m, L.l4_start_abs)) << 16;
-        if (o_want) OS[lane * 21 + 18] |= fold16(o_pseudo + be_sum(o_part + sp_o, o_abs)) << 16;
+        if (o_want) ow[18] |= fold16(o_pseudo + be_sum(o_part + sp_o, o_abs)) << 16;
     }
 
     // 6. records: outer, inner (1-KiB wave stores from the stages), tunnel (16 B per lane)
-    flush_stage(OS, lane, outer, p0, n);
     flush_stage(rec_stage(W), lane, inner, p0, n);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) ow[k] = park[k * kWave + lane];
+    stage_record(W, lane, ow);
+    flush_stage(rec_stage(W), lane, outer, p0, n);
     if (valid) __builtin_nontemporal_store(u32x4{T.w[0], T.w[1], T.w[2], T.w[3]},
                                            reinterpret_cast<u32x4*>(tun) + i);
 }
 
-// One wave per workgroup (as the parse: a CU slot frees when its wave ends); the second
-// record stage (5376 B) puts a wave at 15.1 KB of LDS: 10 waves per CU
+// One wave per workgroup (as the parse: a CU slot frees when its wave ends); 9.7 KB of LDS
+// and 128 VGPRs per wave: 16 waves per CU
 template <bool L4>
 __global__ __launch_bounds__(kWave, 2)
 void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
@@ -421,11 +434,10 @@ void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ outer,
                    rpkt_tun_t* __restrict__ tun, rpkt_rec_t* __restrict__ inner) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch;
-    __shared__ __attribute__((aligned(16))) uint32_t ostage[kWave * 21];
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t p0 = blockIdx.x * kWave;
     if (p0 >= n) return;                                          // wave-uniform exit
-    tunnel_tile<L4>(scratch, ostage, frames, fb, offsets, stride, frame_len, n, flags, outer, tun,
+    tunnel_tile<L4>(scratch, frames, fb, offsets, stride, frame_len, n, flags, outer, tun,
                     inner, p0, lane);
 }
 
