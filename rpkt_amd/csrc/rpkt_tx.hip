@@ -300,8 +300,12 @@ __device__ __forceinline__ void emit_tunnel(uint8_t* t, uint32_t kind, uint32_t 
 // TUN (rpkt_gpu_build_tunnel_batch): a tunnel header from tun[i] composed in the slot too,
 // before the sums (the outer UDP checksum covers it); a GRE checksum filled like an L4 one
 // with no pseudo header.
+#ifndef RPKT_BUILD_MINW
+#define RPKT_BUILD_MINW 3        // waves per SIMD the build compiles for: 3 (132 VGPRs, no
+                                 // spill) beat 4 (128, 12 B of scratch with the tunnel stage)
+#endif
 template <bool L4FILL, bool TUN = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, 4)
+__global__ __launch_bounds__(kWave * kWavesPerBlock, RPKT_BUILD_MINW)
 void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __restrict__ offsets,
                   uint32_t stride, uint32_t frame_len, uint32_t n,
                   const rpkt_rec_t* __restrict__ recs, uint32_t flags, uint8_t* __restrict__ built,
@@ -392,6 +396,13 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         const uint32_t s = be_sum(lds_range_sum(slot, ph + l3, ph + l4), fr.off + l3);
         put_be16(slot + ph + l3 + 10, ~s & 0xffffu);
     }
+    // the write-back's end, taken before the stream so the header layout is not held
+    // across it: the window holds the original bytes around the headers, so the written
+    // range is rounded up to whole 16-B chunks inside the frame (dwordx4 stores)
+    uint32_t hdr_end = far ? l3 + 8u : l4 + fixed4;
+    if (TUN && tkind != RPKT_TUN_NONE && ts + thl > hdr_end) hdr_end = ts + thl;
+    uint32_t r1 = ok ? line_end(fr, hdr_end) : 0u;
+    r1 = far && r1 > l4 ? l4 : r1;                          // the L4 header went to memory
     if constexpr (L4FILL) {
         // everything the checksum needs after the stream is packed into the slot's
         // spare dword (bytes 128..131) and two registers, so the stream keeps its
@@ -442,12 +453,6 @@ void build_kernel(uint8_t* __restrict__ frames, uint32_t fb, const uint32_t* __r
         }
     }
     wave_sync();
-    // the window holds the original bytes around the headers: round the written range
-    // up to whole 16-B chunks inside the frame (dwordx4 stores instead of byte stores)
-    uint32_t hdr_end = far ? l3 + 8u : l4 + fixed4;
-    if (TUN && tkind != RPKT_TUN_NONE && ts + thl > hdr_end) hdr_end = ts + thl;
-    uint32_t r1 = ok ? line_end(fr, hdr_end) : 0u;
-    r1 = far && r1 > l4 ? l4 : r1;                          // the L4 header went to memory
     write_back(rs, frames, W, lane, fr.off, r1);
     if (built && valid) built[i] = ok ? 1 : 0;
 }

@@ -3,7 +3,7 @@ on the GPU box): kernel-time differences of a few percent are below the box-to-b
 spread, so both builds are timed interleaved on the same batch and their outputs are
 compared byte for byte.
 
-Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7|ring2|ringc2|tunnel13]
+Usage: python tools/ab_lib.py <lib_b.so> [--sides AB|A|B] [--leg opts5|optsc5|popts5|poptsc5|parsec2|layers9|forward2|build2|build3|parse2|parse3|chains7|ring2|ringc2|tunnel13|encap13]
 (ring<cfg> / ringc<cfg>: the R rotated batches as one rpkt_gpu_parse_ring[_compact] launch)
                               [--rounds 5] [--launches 20]
 The A side is the in-tree build (rpkt_amd/_build/librpkt_gpu.so).  Build a B side with
@@ -197,6 +197,23 @@ def main():
             keep_alive.append(ws)
             call[name] = (lambda k, L=L, out=out, ws=ws: L.rpkt_gpu_flow_count(
                 ev.data_ptr(), hb.n, 8192, out.data_ptr(), ws.data_ptr(), sp))
+        elif mode == "encap":                       # rpkt_gpu_build_tunnel_batch, in place
+            if "tpar" not in outs:                  # outer records + tunnels, as bench.py
+                pf = args.flags if args.flags is not None else gen.FLAGS.get(cfg, 3)
+                outs["tpar"] = [engine.parse_tunnel_batch(d, pf)[:2] for d in dbs]
+            tpar = outs["tpar"]
+            dbx = [engine.DeviceBatch.from_host(h) for h in hbs]
+            dx = [d.desc() for d in dbx]
+            out = torch.zeros(hb.n, dtype=torch.uint8, device="cuda")
+            keep_alive.append((dbx, dx))
+            L.rpkt_gpu_build_tunnel_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_uint32, ctypes.c_void_p,
+                                                      ctypes.c_void_p]
+            call[name] = (lambda k, L=L, out=out, dx=dx: L.rpkt_gpu_build_tunnel_batch(
+                ctypes.byref(dx[k % R]), tpar[k % R][0].data_ptr(), tpar[k % R][1].data_ptr(), 3,
+                out.data_ptr(), sp))
+            for r, d in enumerate(dbx):
+                outs["%s_frames%d" % (name, r)] = d.frames
         elif mode in ("build", "forward"):          # in place: each side its own frames
             dbx = [engine.DeviceBatch.from_host(h) for h in hbs]
             dx = [d.desc() for d in dbx]
