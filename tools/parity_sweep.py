@@ -9,9 +9,11 @@ difference and names the seed and entry point (a JSON line per seed, progress on
 Per seed: (a) a random packed or strided layout over the captures, configs 2/3/5/6 and
 the dual-stack fuzz (config 12) frames: the parse with a random flag set (with or without
 RPKT_F_IPV6) and flow events, compact records, a two-slot receive ring (80-B and compact),
-both option-walk entry points over full and compact records, the layer walk; (b) a generator batch of a random config and size: the
+both option-walk entry points over full and compact records, the tunnel parse (the pool
+holds tunnel fuzz and tests/tunnel_frames.py frames), the layer walk; (b) a generator batch of a random config and size: the
 build with random checksum flags over its (IPv4 and IPv6) records, the forward with and
-without RPKT_F_IPV6; (c) a fuzzed mbuf-chain batch (configs 8 / 12) through the chain
+without RPKT_F_IPV6, and the encapsulation build over a tunnel batch (configs 13 / 14); (c)
+a fuzzed mbuf-chain batch (configs 8 / 12) through the chain
 parse.  Build and forward rewrite frames in place, so they run on generator batches
 (the random layouts overlap frames on purpose)."""
 import argparse
@@ -29,9 +31,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import oracle  # noqa: E402
 from rpkt_amd import engine, gen  # noqa: E402
 from rpkt_amd.records import (F_FLOW_EV, F_IPV6, LAYERS_DTYPE, as_opts, as_records,  # noqa: E402
-                              as_records16, project16)
+                              as_records16, as_tunnels, project16)
 
 import fuzz_layouts  # noqa: E402
+import tunnel_frames  # noqa: E402
 from test_gpu_parity import assert_same, assert_same16  # noqa: E402
 
 THREADS = min(16, os.cpu_count() or 1)
@@ -45,6 +48,8 @@ def extend_pool():
     if not getattr(extend_pool, "done", False):
         p += fuzz_layouts.frames_of(gen.make_batch(12, 600, seed=121))
         p += fuzz_layouts.frames_of(gen.make_batch(11, 40, seed=111))
+        p += fuzz_layouts.frames_of(gen.make_batch(14, 600, seed=141))     # tunnel fuzz
+        p += tunnel_frames.odd_frames(seed=7, n=200)
         extend_pool.done = True
 
 
@@ -90,6 +95,14 @@ def check_layout(hb, rng):
         assert_same(as_records(rr[k].cpu().numpy()), ok_)
         assert np.array_equal(evs[k].cpu().numpy().view(np.uint64), okev), "ring flow events"
         assert_same16(as_records16(r16[k].cpu().numpy()), project16(ok_, flags))
+    # the tunnel parse (outer, tunnel and inner records) over the same layout
+    tf = int(rng.integers(0, 4)) | (F_IPV6 if rng.random() < 0.5 else 0)
+    go, gt, gi = engine.parse_tunnel_batch(db, tf)
+    oo, ot, oi = oracle.tunnel_batch(hb.frames, hb.n, tf, offsets=hb.offsets, stride=hb.stride,
+                                     frame_len=hb.frame_len)
+    assert_same(as_records(go.cpu().numpy()), oo)
+    assert as_tunnels(gt.cpu().numpy()).tobytes() == ot.tobytes(), "tunnel records"
+    assert_same(as_records(gi.cpu().numpy()), oi)
     gl = engine.layers_batch(db).cpu().numpy().view(LAYERS_DTYPE)
     ol = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets, stride=hb.stride,
                              frame_len=hb.frame_len)
@@ -126,6 +139,28 @@ def check_tx(rng, seed):
     return {"cfg": cfg, "n": n, "build_flags": bflags, "fwd_flags": ff}
 
 
+def check_encap(rng, seed):
+    """The encapsulation build over a tunnel generator batch: outer records and tunnel
+    records from the oracle's tunnel parse, random checksum flags."""
+    import torch
+    cfg = int(rng.choice([13, 14]))
+    n = int(rng.integers(1, 20000))
+    hb = gen.make_batch(cfg, n, seed=seed)
+    tf = 3 | (F_IPV6 if rng.random() < 0.5 else 0)
+    oo, ot, _ = oracle.tunnel_batch(hb.frames, hb.n, tf, offsets=hb.offsets, stride=hb.stride,
+                                    frame_len=hb.frame_len)
+    bflags = int(rng.integers(0, 4))
+    db = engine.DeviceBatch.from_host(hb)
+    d = torch.from_numpy(np.ascontiguousarray(oo).view(np.uint8).copy()).cuda()
+    t = torch.from_numpy(np.ascontiguousarray(ot).view(np.uint8).copy()).cuda()
+    gb = engine.build_tunnel_batch(db, d, t, bflags).cpu().numpy()
+    o, ob = oracle.build_tunnel_batch(hb.frames, hb.n, oo, ot, bflags, offsets=hb.offsets,
+                                      stride=hb.stride, frame_len=hb.frame_len)
+    assert np.array_equal(gb, ob), "encap built flags"
+    assert np.array_equal(db.frames.cpu().numpy()[:o.size], o), "encap frames"
+    return {"cfg": cfg, "n": n, "flags": bflags}
+
+
 def check_chains(rng, seed):
     cfg = int(rng.choice([8, 12]))
     hc = gen.make_chains(cfg, n=int(rng.integers(1, 20000)), layout="fuzz", seed=seed)
@@ -156,6 +191,8 @@ def main():
                 rec["layout"] = check_layout(hb, rng)
                 step = "tx"
                 rec["tx"] = check_tx(rng, seed)
+                step = "encap"
+                rec["encap"] = check_encap(rng, seed)
                 step = "chains"
                 rec["chains"] = check_chains(rng, seed)
             except AssertionError as e:
