@@ -1074,7 +1074,33 @@ def run_tx(cfg, mode, args, rank, world):
         alg = int(lens.sum()) + hbs[0].n + int((r["l4_off"][kept].astype(np.int64) + 8).sum())
     achieved = alg / (kern_ms / 1e3) / 1e9
     traffic, tsrc = pmc_traffic_tx("%s%d" % (mode, cfg), hbs[0].n)   # the bench leg's name
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.tx_cpu_seconds > 0:
+        # the leg's CPU restatement beside it: the oracle over the batch's first frames
+        # (<= 64 MB), 1 thread, outputs allocated once outside the timed calls
+        oracle, build = oracle_for_baseline()
+        hs = head_sample(hbs[0], 64 << 20)
+        m = hs.n
+        kw = dict(offsets=hs.offsets, stride=hs.stride, frame_len=hs.frame_len)
+        if mode == "encap":
+            kw.update(recs=as_records(tpar[0][0].cpu().numpy())[:m],
+                      tun=as_tunnels(tpar[0][1].cpu().numpy())[:m], flags=3)
+        elif mode == "tunnel":
+            kw.update(flags=pflags)
+        elif mode == "fields":
+            kw.update(layers=lays[0].cpu().numpy().view(LAYERS_DTYPE)[:m], reqs=reqs)
+        elif mode == "forward":
+            kw.update(recs=r[:m], flags=fwd_flags, dmac=dmac, smac=smac,
+                      forbid=[ip_u32(x) for x in FORBID_IPS])
+        elif mode != "layers":
+            kw.update(recs=r[:m], flags=3)
+        reps, dt = timed_reps(oracle.leg_callable(mode, hs.frames, m, **kw), args.tx_cpu_seconds)
+        cpu = {"value": round(m * reps / dt / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+               "sample": "%d reps x first %d frames (%.0f MB) of the batch, 1 thread"
+                         % (reps, m, hs.lens().sum() / 1e6),
+               "seconds": round(dt, 2), "build": build}
     return {"mpps": hbs[0].n * world * args.steps / wall / 1e6, "kernel_ms": kern_ms,
+            "cpu_baseline": cpu,
             "ms_per_step": wall / args.steps * 1e3, "frames_per_rank": hbs[0].n,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -1128,6 +1154,8 @@ def leg_summary(v):
                   "flow_reduce_via", "flow_reduce_verified"):
             if k in v:
                 s[k] = _r(v[k], 3)
+        if isinstance(v.get("cpu_baseline"), dict) and "value" in v["cpu_baseline"]:
+            s["cpu_mpps"] = v["cpu_baseline"]["value"]        # the oracle, 1 thread
         return s
     if "ns_per_pkt" in v:                                          # config 1 (host CPU)
         return {"ns_per_pkt": v["ns_per_pkt"], "mpps": v["mpps"], "cores": v["cores"]}
@@ -1243,6 +1271,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="all-cores CPU leg threads (0 = every usable host thread)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tx-cpu-seconds", type=float, default=1.5,
+                    help="per TX / walk / tunnel leg: the oracle's 1-thread timing beside it "
+                         "(0: off)")
     ap.add_argument("--tx", default=None,
                     help="legs beyond the parse reported under 'extra' (default "
                          "build2,build3,forward2,opts5,optsc5,layers9,fields9; none at N>1) (build<cfg>, "

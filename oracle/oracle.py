@@ -375,6 +375,67 @@ def fields_batch(frames, n, layers, reqs, offsets=None, stride=0, frame_len=0):
     return values, present
 
 
+def leg_callable(mode, frames, n, offsets=None, stride=0, frame_len=0, recs=None, tun=None,
+                 layers=None, reqs=None, flags=3, dmac=b"", smac=b"", forbid=()):
+    """A closure that runs one bench leg's CPU restatement over a host sample with every
+    output allocated here, once, and its C arguments converted once (bench.py's per-leg
+    cpu_baseline times the closure alone: no allocation per call).  mode: build / forward
+    / encap (in place on a private copy of the frames, which each call rewrites again),
+    opts / optsc (both: Ipv4OptionsIter + TcpOptionsIter from full records), layers,
+    fields, tunnel.  The closure's `arrays` attribute holds its buffers."""
+    from rpkt_amd.records import FIELD_REQ_DTYPE, LAYERS_DTYPE, OPTS_DTYPE, REC_DTYPE, TUN_DTYPE
+    L = lib()
+    src = np.ascontiguousarray(frames, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint32) if offsets is not None else None
+    head = (src, offs, stride, frame_len, n)
+    if mode in ("build", "forward", "encap"):
+        buf = src.copy()
+        done = np.zeros(n, dtype=np.uint8)
+        r = np.ascontiguousarray(recs)
+        head = (buf, offs, stride, frame_len, n)
+        if mode == "build":
+            fn, arrays, rest = L.oracle_build_batch, [buf, done, r], (r, flags, done)
+        elif mode == "encap":
+            t = np.ascontiguousarray(tun)
+            fn, arrays, rest = L.oracle_build_tunnel_batch, [buf, done, r, t], (r, t, flags, done)
+        else:
+            fb = np.ascontiguousarray(np.sort(np.asarray(forbid, dtype=np.uint32)))
+            dm = np.frombuffer(bytes(dmac), dtype=np.uint8).copy()
+            sm = np.frombuffer(bytes(smac), dtype=np.uint8).copy()
+            fn, arrays = L.oracle_forward_batch, [buf, done, r, fb, dm, sm]
+            rest = (r, dm, sm, fb if fb.size else None, fb.size, done, flags)
+    elif mode in ("opts", "optsc"):
+        r = np.ascontiguousarray(recs)
+        out = np.zeros(n, dtype=OPTS_DTYPE)
+        fn, arrays, rest = L.oracle_options_batch, [r, out], (r, out)
+    elif mode == "layers":
+        out = np.zeros(n, dtype=LAYERS_DTYPE)
+        fn, arrays, rest = L.oracle_layers_batch, [out], (out,)
+    elif mode == "fields":
+        lay = np.ascontiguousarray(layers, dtype=LAYERS_DTYPE)
+        q = np.ascontiguousarray(reqs, dtype=FIELD_REQ_DTYPE)
+        values = np.zeros((n, q.size), dtype=np.uint64)
+        present = np.zeros(n, dtype=np.uint32)
+        fn, arrays, rest = L.oracle_fields_batch, [lay, q, values, present], \
+            (lay, q, q.size, values, present)
+    elif mode == "tunnel":
+        outer = np.zeros(n, dtype=REC_DTYPE)
+        tu = np.zeros(n, dtype=TUN_DTYPE)
+        inner = np.zeros(n, dtype=REC_DTYPE)
+        fn, arrays, rest = L.oracle_tunnel_batch, [outer, tu, inner], (flags, outer, tu, inner)
+    else:
+        raise ValueError("leg_callable: unknown mode %r" % mode)
+    # (frames, frames bytes, offsets, stride, frame_len, n, ...) as C arguments, once
+    conv = lambda x: _ptr(x) if isinstance(x, np.ndarray) else x      # noqa: E731
+    args = (conv(head[0]), head[0].size, _ptr(head[1]), head[2], head[3], head[4]) + \
+        tuple(conv(x) for x in rest)
+
+    def run():
+        fn(*args)
+    run.arrays = [src, offs] + arrays
+    return run
+
+
 def flow_count(ev, n_buckets):
     ev = np.ascontiguousarray(ev, dtype=np.uint64)
     counters = np.zeros((n_buckets + 1) * 4, dtype=np.uint64)

@@ -180,3 +180,54 @@ def test_packet_l4_all_cores_agrees():
     one = oracle.packet_l4_loop(f, hb.n, hb.stride, flen, 2, want)
     assert one == 2
     assert oracle.packet_l4_loop_mt(f, hb.n, hb.stride, flen, 2, want, 4) == 4 * one
+
+
+@pytest.mark.parametrize("mode,cfg", [("build", 3), ("forward", 2), ("opts", 5), ("layers", 9),
+                                      ("fields", 9), ("tunnel", 13), ("encap", 13)])
+def test_tx_leg_cpu_callable(mode, cfg):
+    """The per-leg CPU timing's body (oracle.leg_callable): after the untimed first call a
+    call allocates nothing (tracemalloc), and its outputs are the oracle's own (the in-place
+    legs rebuild their private copy identically on every call)."""
+    import tracemalloc
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import bench
+    from oracle import oracle
+    from rpkt_amd import fields, gen
+    hb = gen.make_mix(600, seed=9) if cfg == 9 else gen.make_batch(cfg, 600)
+    kw = dict(offsets=hb.offsets, stride=hb.stride, frame_len=hb.frame_len)
+    r = oracle.parse_batch(hb.frames, hb.n, flags=gen.FLAGS.get(cfg, 3) | 3, **kw)
+    extra = {}
+    if mode in ("build", "opts"):
+        extra = dict(recs=r, flags=3)
+    elif mode == "forward":
+        extra = dict(recs=r, flags=0, dmac=b"\xaa" * 6, smac=b"\xbb" * 6, forbid=[1, 2, 3])
+    elif mode == "fields":
+        extra = dict(layers=oracle.layers_batch(hb.frames, hb.n, **kw),
+                     reqs=fields.requests(bench.FIELD_LEG))
+    elif mode == "tunnel":
+        extra = dict(flags=3)
+    elif mode == "encap":
+        o, t, _ = oracle.tunnel_batch(hb.frames, hb.n, 3, **kw)
+        extra = dict(recs=o, tun=t, flags=3)
+    fn = oracle.leg_callable(mode, hb.frames, hb.n, **kw, **extra)
+    fn()
+    tracemalloc.start()
+    try:
+        base = tracemalloc.get_traced_memory()[0]
+        tracemalloc.reset_peak()
+        for _ in range(3):
+            fn()
+        cur, peak = tracemalloc.get_traced_memory()
+    finally:
+        tracemalloc.stop()
+    assert peak - base < 4096 and abs(cur - base) < 4096, (peak - base, cur - base)
+    got = fn.arrays
+    if mode == "build":                       # the closure's private copy, built in place
+        out, _ = oracle.build_batch(hb.frames, hb.n, r, 3, **kw)
+        assert got[2].tobytes() == out.tobytes()
+    elif mode == "tunnel":
+        want = oracle.tunnel_batch(hb.frames, hb.n, 3, **kw)
+        assert all(g.tobytes() == w.tobytes() for g, w in zip(got[2:], want))
+    elif mode == "layers":
+        assert got[2].tobytes() == oracle.layers_batch(hb.frames, hb.n, **kw).tobytes()

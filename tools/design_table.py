@@ -79,8 +79,11 @@ def table(d):
                      lambda x: "—" if x is None else "%.3f" % x)
         bold = label.startswith("**")
         fr = cell(frac, lambda x: ("**%.2f**" if bold else "%.2f") % x)
-        out.append("| %s | %s | %s | %s | %s |" % (
-            label, cell(alg, fmt_bytes), cell(ms, lambda x: "%.1f µs" % (x * 1e3)), fr, ratio))
+        cpu = [(v.get("cpu_baseline") or {}).get("value") for v in legs]
+        cpu_c = cell(cpu, lambda x: "—" if x is None else "%.1f" % x)
+        out.append("| %s | %s | %s | %s | %s | %s |" % (
+            label, cell(alg, fmt_bytes), cell(ms, lambda x: "%.1f µs" % (x * 1e3)), fr, ratio,
+            cpu_c))
     return out
 
 
@@ -92,7 +95,8 @@ def main(path, print_only=False):
         s = open(p).read()
         i = s.index("| leg | alg. bytes / launch |")
         j = s.index("\n\n", i)
-        hdr = s[i:s.index("\n", s.index("\n", i) + 1) + 1]
+        hdr = ("| leg | alg. bytes / launch | kernel | frac of 8 TB/s | PMC traffic / alg. | "
+               "oracle, 1 thread (Mpps) |\n|---|---|---|---|---|---|\n")
         s = s[:i] + hdr + "\n".join(rows) + s[j:]
         open(p, "w").write(s)
     print("\n".join(rows))
