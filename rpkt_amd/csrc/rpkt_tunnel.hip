@@ -6,19 +6,19 @@
 // One wavefront per tile, as parse_kernel: the outer header windows go to LDS (on long
 // tiles together with each frame's tail line, whose sum is taken there and then) and each
 // lane runs parse_lane on its frame; the lane then decodes the tunnel header(s) from the
-// same window (FrameDw: global memory past it), the outer record waits in registers (its
+// same window (FrameDw: global memory past it).  The outer record waits in registers (its
 // words 0..11 in LDS past the inner record's stage once that is written: 128 VGPRs and
 // 9.7 KB of LDS per wave, 16 waves per CU), and the inner frame's window is made from the
-// outer one: the chunks they
-// share move down the lane's slot and only the chunks past the outer window are loaded.
-// parse_lane runs again from the inner frame's first byte (its IP header for GTP-U and
-// GRE).  One flattened chunk stream (rpkt_common.h) then sums each lane's main range --
-// the inner L4 bytes past the inner window, or the outer L4 range without a tunnel -- and
-// the outer L4 sum (UDP, or GRE with its checksum), whose range contains the inner one,
-// is composed from the outer window's part, the inner window's part (LDS), the main
-// stream's sum when the rest of the two ranges is the same, and a rare stream for bytes
-// before the inner window or a trailer after the inner packet.  Each payload byte leaves
-// HBM about once for all four sums (PMC reads 1.04x the frame bytes on config 13).
+// outer one: the chunks they share move down the lane's slot and only the chunks past the
+// outer window are loaded.  parse_lane runs again from the inner frame's first byte (its
+// IP header for GTP-U and GRE).  One flattened chunk stream (rpkt_common.h) then sums each
+// lane's main range -- the inner L4 bytes past the inner window, or the outer L4 range
+// without a tunnel -- and the outer L4 sum (UDP, or GRE with its checksum), whose range
+// contains the inner one, is composed from the outer window's part, the inner window's
+// part (LDS), the main stream's sum when the rest of the two ranges is the same, and a
+// rare stream for bytes before the inner window or a trailer after the inner packet.
+// Each payload byte leaves HBM about once for all four sums (config 13: reads 1.09x the
+// frame bytes, the excess the line the outer window ends in).
 #include "rpkt_common.h"
 
 namespace {
@@ -415,7 +415,8 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W,
         if (o_want) ow[18] |= fold16(o_pseudo + be_sum(o_part + sp_o, o_abs)) << 16;
     }
 
-    // 6. records: outer, inner (1-KiB wave stores from the stages), tunnel (16 B per lane)
+    // 6. records: the inner one, then the outer one staged where it was (1-KiB wave stores),
+    // the tunnel record (16 B per lane)
     flush_stage(rec_stage(W), lane, inner, p0, n);
 #pragma unroll
     for (int k = 0; k < 12; ++k) ow[k] = park[k * kWave + lane];
