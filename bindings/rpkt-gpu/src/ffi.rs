@@ -344,7 +344,9 @@ extern "C" {
 
     pub fn rpkt_gpu_parse_tunnel_batch(batch: *const rpkt_batch_t, flags: u32,
                                        outer_dev: *mut rpkt_rec_t, tun_dev: *mut rpkt_tun_t,
-                                       inner_dev: *mut rpkt_rec_t, stream: *mut c_void) -> c_int;
+                                       inner_dev: *mut rpkt_rec_t,
+                                       flow_ev_dev: *mut rpkt_flow_ev_t, n_buckets: u32,
+                                       stream: *mut c_void) -> c_int;
     pub fn rpkt_gpu_build_tunnel_batch(batch: *const rpkt_batch_t, recs_dev: *const rpkt_rec_t,
                                        tun_dev: *const rpkt_tun_t, flags: u32, built_dev: *mut u8,
                                        stream: *mut c_void) -> c_int;

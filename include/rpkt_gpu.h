@@ -468,12 +468,19 @@ typedef struct rpkt_tun {
  *                 the OUTER frame (rpkt's Cursor::cursor() of the inner views) and
  *                 frame_len = the inner frame's length; status RPKT_S_NO_INNER (all else
  *                 0) when tun_dev[i].status != RPKT_T_OK.
- * flags: RPKT_F_IP_SUM, RPKT_F_L4_SUM, RPKT_F_IPV6, applied to both levels (no flow
- * events).  Each byte is read from HBM about once: the outer L4 sum (UDP, or GRE with
- * its checksum) reuses the inner L4 sum's stream over the bytes the two share.
- * outer_dev / inner_dev n * 80 B, tun_dev n * 16 B, all 16-byte aligned. */
+ * flags: RPKT_F_IP_SUM, RPKT_F_L4_SUM, RPKT_F_IPV6, applied to both levels, and
+ * RPKT_F_FLOW_EV: flow_ev_dev[i] (n * 8 B, 8-byte aligned; n_buckets 1..
+ * RPKT_FLOW_MAX_BUCKETS) is the flow event of the INNER record when the tunnel decoded
+ * (tun_dev[i].status == RPKT_T_OK: the inner 5-tuple, the inner frame's length, the inner
+ * sums' bad bits -- per-subscriber / per-tenant accounting of the overlay through
+ * rpkt_gpu_flow_count and rpkt_gpu_flow_reduce), else of the outer record, exactly as
+ * rpkt_gpu_parse_batch forms it from a record.  Each byte is read from HBM about once:
+ * the outer L4 sum (UDP, or GRE with its checksum) reuses the inner L4 sum's stream over
+ * the bytes the two share.  outer_dev / inner_dev n * 80 B, tun_dev n * 16 B, all
+ * 16-byte aligned. */
 int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* batch, uint32_t flags, rpkt_rec_t* outer_dev,
-                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev, void* stream);
+                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev,
+                                rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
 
 /* ---- TX side ---------------------------------------------------------------- */
 

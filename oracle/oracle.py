@@ -135,6 +135,9 @@ def lib():
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]
         L.oracle_tunnel_batch.restype = None
+        L.oracle_tunnel_flow_events.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_tunnel_flow_events.restype = None
         L.oracle_layers_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_void_p]
@@ -341,6 +344,16 @@ def tunnel_batch(frames, n, flags=3, offsets=None, stride=0, frame_len=0):
     lib().oracle_tunnel_batch(_ptr(frames), frames.size, _ptr(offs), stride, frame_len, n, flags,
                               _ptr(outer), _ptr(tun), _ptr(inner))
     return outer, tun, inner
+
+
+def tunnel_flow_events(outer, tun, inner, n_buckets):
+    """rpkt_gpu_parse_tunnel_batch's RPKT_F_FLOW_EV events from its three record arrays:
+    the inner record's event when the tunnel decoded, else the outer record's."""
+    outer, tun, inner = (np.ascontiguousarray(x) for x in (outer, tun, inner))
+    ev = np.zeros(outer.size, dtype=np.uint64)
+    lib().oracle_tunnel_flow_events(_ptr(outer), _ptr(tun), _ptr(inner), outer.size, n_buckets,
+                                    _ptr(ev))
+    return ev
 
 
 def tunnel_one(frame, flags=3):

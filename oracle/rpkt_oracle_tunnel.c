@@ -16,6 +16,7 @@
 #include "../include/rpkt_gpu.h"
 
 void oracle_parse_one(const uint8_t* frame, uint32_t frame_len, uint32_t flags, rpkt_rec_t* rec);
+uint64_t oracle_flow_event(const rpkt_rec_t* r, uint32_t n_buckets);
 void oracle_parse_at_ip(const uint8_t* frame, uint32_t frame_len, uint32_t flags, uint16_t et,
                         rpkt_rec_t* rec);
 int oracle_rec_is_ip6(const rpkt_rec_t* r);
@@ -267,4 +268,13 @@ void oracle_tunnel_batch(const uint8_t* frames, uint64_t frames_bytes, const uin
         if (off + len > frames_bytes) len = frames_bytes - off;
         oracle_tunnel_one(frames + off, (uint32_t)len, flags, &outer[i], &tun[i], &inner[i]);
     }
+}
+
+/* The flow event rpkt_gpu_parse_tunnel_batch writes with RPKT_F_FLOW_EV: the inner
+ * record's when the tunnel decoded, else the outer record's (include/rpkt_gpu.h). */
+void oracle_tunnel_flow_events(const rpkt_rec_t* outer, const rpkt_tun_t* tun,
+                               const rpkt_rec_t* inner, uint32_t n, uint32_t n_buckets,
+                               uint64_t* ev) {
+    for (uint32_t i = 0; i < n; i++)
+        ev[i] = oracle_flow_event(tun[i].status == RPKT_T_OK ? &inner[i] : &outer[i], n_buckets);
 }

@@ -300,6 +300,23 @@ __device__ __forceinline__ void inner_window_reuse(__amdgpu_buffer_rsrc_t rs, ui
     wave_sync();
 }
 
+// The flow event of a record from its words alone (its status is byte 0; the IPv6 block
+// is used when the dispatch ethertype -- the last tag's, or the frame's, or an inner IP
+// packet's start type -- is 0x86DD and the IPv6 header was reached), as flow_event forms it.
+template <typename WordsT>
+__device__ __forceinline__ uint64_t record_event(const WordsT& w, uint32_t n_buckets) {
+    LaneRec R;
+    R.status = w[0] & 0xffu;
+    const uint32_t nv = (w[0] >> 8) & 0xffu;
+    const uint32_t det = nv == 0u ? w[0] >> 16 : (nv == 1u ? w[5] & 0xffffu : w[5] >> 16);
+    R.is6 = det == 0x86ddu && R.status != RPKT_S_ETH_SHORT && R.status != RPKT_S_VLAN_SHORT &&
+            R.status != RPKT_S_NOT_IPV4;
+    uint32_t x[20];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) x[k] = w[k];
+    return flow_event(R, x, n_buckets);
+}
+
 // chunk loads in flight per lane in the main stream (6 and 8 measured: no gain, and 8 costs
 // occupancy)
 #ifndef RPKT_TUN_UNROLL
@@ -313,7 +330,9 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W,
                                             const uint32_t* __restrict__ offsets, uint32_t stride,
                                             uint32_t frame_len, uint32_t n, uint32_t flags,
                                             rpkt_rec_t* __restrict__ outer, rpkt_tun_t* __restrict__ tun,
-                                            rpkt_rec_t* __restrict__ inner, uint32_t p0, int lane) {
+                                            rpkt_rec_t* __restrict__ inner,
+                                            uint64_t* __restrict__ flow_ev, uint32_t n_buckets,
+                                            uint32_t p0, int lane) {
     const uint32_t i = p0 + lane;
     const bool valid = i < n;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(frames, fb);
@@ -416,10 +435,15 @@ __device__ __forceinline__ void tunnel_tile(WaveScratch& W,
     }
 
     // 6. records: the inner one, then the outer one staged where it was (1-KiB wave stores),
-    // the tunnel record (16 B per lane)
+    // the tunnel record (16 B per lane); the flow event from the inner record when the
+    // tunnel decoded, else from the outer one (include/rpkt_gpu.h)
+    const bool ev = (flags & RPKT_F_FLOW_EV) && valid;
+    if (ev && T.ok) __builtin_nontemporal_store(record_event(rec_stage(W) + lane * 21, n_buckets),
+                                                &flow_ev[i]);
     flush_stage(rec_stage(W), lane, inner, p0, n);
 #pragma unroll
     for (int k = 0; k < 12; ++k) ow[k] = park[k * kWave + lane];
+    if (ev && !T.ok) __builtin_nontemporal_store(record_event(ow, n_buckets), &flow_ev[i]);
     stage_record(W, lane, ow);
     flush_stage(rec_stage(W), lane, outer, p0, n);
     if (valid) __builtin_nontemporal_store(u32x4{T.w[0], T.w[1], T.w[2], T.w[3]},
@@ -433,13 +457,14 @@ __global__ __launch_bounds__(kWave, 2)
 void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                    const uint32_t* __restrict__ offsets, uint32_t stride, uint32_t frame_len,
                    uint32_t n, uint32_t flags, rpkt_rec_t* __restrict__ outer,
-                   rpkt_tun_t* __restrict__ tun, rpkt_rec_t* __restrict__ inner) {
+                   rpkt_tun_t* __restrict__ tun, rpkt_rec_t* __restrict__ inner,
+                   uint64_t* __restrict__ flow_ev, uint32_t n_buckets) {
     __shared__ __attribute__((aligned(16))) WaveScratch scratch;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t p0 = blockIdx.x * kWave;
     if (p0 >= n) return;                                          // wave-uniform exit
     tunnel_tile<L4>(scratch, frames, fb, offsets, stride, frame_len, n, flags, outer, tun,
-                    inner, p0, lane);
+                    inner, flow_ev, n_buckets, p0, lane);
 }
 
 }  // namespace
@@ -447,9 +472,15 @@ void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
 extern "C" {
 
 int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_t* outer_dev,
-                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev, void* stream) {
+                                rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev,
+                                rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!b) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_IPV6)) return RPKT_E_INVAL;
+    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_IPV6 | RPKT_F_FLOW_EV))
+        return RPKT_E_INVAL;
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS) return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
+    }
     if (b->n == 0) return RPKT_OK;
     if (!b->frames_dev || !outer_dev || !tun_dev || !inner_dev) return RPKT_E_INVAL;
     if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
@@ -460,7 +491,7 @@ int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_
     auto k = (flags & RPKT_F_L4_SUM) ? tunnel_kernel<true> : tunnel_kernel<false>;
     return launch(k, dim3(grid), dim3(kWave), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags, outer_dev,
-                  tun_dev, inner_dev);
+                  tun_dev, inner_dev, (uint64_t*)flow_ev_dev, n_buckets);
 }
 
 }  // extern "C"

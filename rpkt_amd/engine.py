@@ -135,7 +135,8 @@ def lib():
         L.rpkt_gpu_parse_options_batch_compact.restype = ctypes.c_int
         L.rpkt_gpu_parse_tunnel_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_uint32,
                                                   ctypes.c_void_p, ctypes.c_void_p,
-                                                  ctypes.c_void_p, ctypes.c_void_p]
+                                                  ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_uint32, ctypes.c_void_p]
         L.rpkt_gpu_parse_tunnel_batch.restype = ctypes.c_int
         L.rpkt_gpu_build_tunnel_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_uint32,
@@ -265,19 +266,25 @@ def parse_batch(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=Non
     return (recs, flow_ev) if flags & F_FLOW_EV else recs
 
 
-def parse_tunnel_batch(batch, flags=3, outer=None, tun=None, inner=None, stream=None):
+def parse_tunnel_batch(batch, flags=3, outer=None, tun=None, inner=None, stream=None,
+                       flow_ev=None, n_buckets=0):
     """rpkt_gpu_parse_tunnel_batch: returns (outer records, rpkt_tun_t, inner records) as
-    uint8 tensors (n * 80, n * 16, n * 80 bytes)."""
+    uint8 tensors (n * 80, n * 16, n * 80 bytes); with RPKT_F_FLOW_EV also the flow events
+    (int64 tensor of n: the inner record's event when the tunnel decoded, else the outer's)."""
     torch = _torch()
     dev = batch.frames.device
     outer = alloc_records(batch.n, dev) if outer is None else outer
     inner = alloc_records(batch.n, dev) if inner is None else inner
     tun = torch.empty(batch.n * 16, dtype=torch.uint8, device=dev) if tun is None else tun
+    if flags & F_FLOW_EV and flow_ev is None:
+        flow_ev = torch.empty(batch.n, dtype=torch.int64, device=dev)
     d = batch.desc()
     rc = lib().rpkt_gpu_parse_tunnel_batch(ctypes.byref(d), flags, outer.data_ptr(),
-                                           tun.data_ptr(), inner.data_ptr(), _stream_ptr(stream))
+                                           tun.data_ptr(), inner.data_ptr(),
+                                           flow_ev.data_ptr() if flow_ev is not None else None,
+                                           n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_tunnel_batch")
-    return outer, tun, inner
+    return (outer, tun, inner, flow_ev) if flags & F_FLOW_EV else (outer, tun, inner)
 
 
 def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):

@@ -106,7 +106,32 @@ def test_tunnel_empty_batch_and_validation(torch):
     engine.parse_tunnel_batch(db, 3)                           # n == 0: nothing launched
     db.n = 1
     with pytest.raises(engine.RpktError):
-        engine.parse_tunnel_batch(db, 4)                       # FLOW_EV is not supported
+        engine.parse_tunnel_batch(db, 4)                       # FLOW_EV needs n_buckets
+    with pytest.raises(engine.RpktError):
+        engine.parse_tunnel_batch(db, 3 | 16)                  # an unknown flag
+
+
+@pytest.mark.parametrize("cfg,n,nb", [(13, None, 8192), (14, 1 << 15, 977), (14, 4099, 1)])
+def test_tunnel_flow_events(torch, cfg, n, nb):
+    """RPKT_F_FLOW_EV on the tunnel parse: every event equals the oracle's (the inner
+    record's event when the tunnel decoded, else the outer's), the records are those of
+    the call without events, and rpkt_gpu_flow_count over them gives the oracle's
+    per-inner-flow counters."""
+    hb = gen.make_batch(cfg, n)
+    fl = gen.FLAGS.get(cfg, 3)
+    db = engine.DeviceBatch.from_host(hb)
+    go, gt, gi, ev = engine.parse_tunnel_batch(db, fl | 4, n_buckets=nb)
+    oo, ot, oi = check_tunnel(hb, fl)
+    assert as_records(go.cpu().numpy()).tobytes() == oo.tobytes()
+    assert as_records(gi.cpu().numpy()).tobytes() == oi.tobytes()
+    want = oracle.tunnel_flow_events(oo, ot, oi, nb)
+    got = ev.cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, want), int(np.nonzero(got != want)[0][0])
+    c = engine.flow_count(ev, hb.n, nb).cpu().numpy().view(np.uint64)
+    assert np.array_equal(c, oracle.flow_count(want, nb))
+    if cfg == 13:                                 # the inner flows are counted, not the outer
+        inner_ok = (ot["status"] == TUN_STATUS["OK"]) & (oi["status"] == STATUS["OK"])
+        assert inner_ok.mean() > 0.97 and c.reshape(-1, 4)[:nb, 0].sum() >= inner_ok.sum()
 
 
 @pytest.mark.parametrize("lead", list(range(16)))

@@ -178,3 +178,22 @@ def test_odd_tunnel_frames_decode():
     assert int(t["kind"]) == TUN_KIND["NONE"]                 #   (outer IPv6 too)
     o, t, i = oracle.tunnel_one(frames[1], 3)
     assert int(o["n_vlan"]) == 2 and int(t["status"]) == TUN_STATUS["OK"]
+
+
+def test_tunnel_flow_events_are_the_inner_or_outer_record_events():
+    """oracle.tunnel_flow_events: a frame without a decoded tunnel gets exactly
+    rpkt_gpu_parse_batch's event of its outer record; a tunnel frame the event of its inner
+    record (its 5-tuple and length), which differs from the outer one."""
+    from rpkt_amd import gen
+    hb = gen.make_batch(14, 3000, seed=77)
+    o, t, i = oracle.tunnel_batch(hb.frames, hb.n, F6, offsets=hb.offsets, stride=hb.stride,
+                                  frame_len=hb.frame_len)
+    ev = oracle.tunnel_flow_events(o, t, i, 8192)
+    _, pev = oracle.parse_batch(hb.frames, hb.n, flags=F6, offsets=hb.offsets, stride=hb.stride,
+                                frame_len=hb.frame_len, n_buckets=8192, flow_ev=True)
+    tun = t["status"] == TUN_STATUS["OK"]
+    assert tun.any() and (~tun).any()
+    assert np.array_equal(ev[~tun], pev[~tun])
+    assert np.array_equal(ev[tun] & 0xffffffff, i["frame_len"][tun].astype(np.uint64))
+    assert (ev[tun] != pev[tun]).mean() > 0.9
+

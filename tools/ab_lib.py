@@ -115,14 +115,15 @@ def main():
         elif mode == "tunnel":                      # rpkt_gpu_parse_tunnel_batch, all sums
             fn = L.rpkt_gpu_parse_tunnel_batch
             fn.argtypes = [P, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                           ctypes.c_void_p]
+                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
             rec = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
             tun = torch.zeros(hb.n * 16, dtype=torch.uint8, device="cuda")
             out = torch.zeros(hb.n * 80, dtype=torch.uint8, device="cuda")
             outs[name + "_outer"], outs[name + "_tun"] = rec, tun
             flags = args.flags if args.flags is not None else gen.FLAGS.get(cfg, 3)
             call[name] = (lambda k, fn=fn, out=out, rec=rec, tun=tun, flags=flags: fn(
-                ctypes.byref(descs[k % R]), flags, rec.data_ptr(), tun.data_ptr(), out.data_ptr(), sp))
+                ctypes.byref(descs[k % R]), flags, rec.data_ptr(), tun.data_ptr(), out.data_ptr(),
+                None, 0, sp))
         elif mode == "layers":
             L.rpkt_gpu_layers_batch.argtypes = [P, ctypes.c_void_p, ctypes.c_void_p]
             out = torch.zeros(hb.n * 64, dtype=torch.uint8, device="cuda")

@@ -97,12 +97,14 @@ def check_layout(hb, rng):
         assert_same16(as_records16(r16[k].cpu().numpy()), project16(ok_, flags))
     # the tunnel parse (outer, tunnel and inner records) over the same layout
     tf = int(rng.integers(0, 4)) | (F_IPV6 if rng.random() < 0.5 else 0)
-    go, gt, gi = engine.parse_tunnel_batch(db, tf)
+    go, gt, gi, gev = engine.parse_tunnel_batch(db, tf | F_FLOW_EV, n_buckets=nb)
     oo, ot, oi = oracle.tunnel_batch(hb.frames, hb.n, tf, offsets=hb.offsets, stride=hb.stride,
                                      frame_len=hb.frame_len)
     assert_same(as_records(go.cpu().numpy()), oo)
     assert as_tunnels(gt.cpu().numpy()).tobytes() == ot.tobytes(), "tunnel records"
     assert_same(as_records(gi.cpu().numpy()), oi)
+    assert np.array_equal(gev.cpu().numpy().view(np.uint64),
+                          oracle.tunnel_flow_events(oo, ot, oi, nb)), "tunnel flow events"
     gl = engine.layers_batch(db).cpu().numpy().view(LAYERS_DTYPE)
     ol = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets, stride=hb.stride,
                              frame_len=hb.frame_len)
