@@ -179,9 +179,10 @@ class EtherFrame:
         return int(self.rec["ethertype"])
 
     def payload(self):
-        """ether/generated.rs:63-67 — advance(14)."""
+        """ether/generated.rs:63-67 — advance(14) (from the cursor: an inner frame of a
+        tunnel starts past the outer headers, rpkt_amd.tunviews)."""
         b = self.buf
-        return Cursor(b.rec, b.frame, "l3", 0, 14, b.length - 14)
+        return Cursor(b.rec, b.frame, "l3", 0, b.off + 14, b.length - 14)
 
 
 class EtherDot3Frame:

@@ -154,8 +154,10 @@ def test_cpu_baseline_timed_call_allocates_nothing(threads):
         cur, peak = tracemalloc.get_traced_memory()
     finally:
         tracemalloc.stop()
+    # (a few KiB of interpreter objects may come and go; a record-sized buffer per call
+    # would be 320 KiB here)
     assert peak - base < rec_bytes // 20, (peak - base, rec_bytes)
-    assert abs(cur - base) < 4096, (cur, base)
+    assert abs(cur - base) < rec_bytes // 20, (cur, base)
     want = oracle.parse_batch(hb.frames, hb.n, flags=gen.FLAGS[2], stride=hb.stride,
                               frame_len=hb.frame_len)
     assert fn.out.tobytes() == want.tobytes()
@@ -221,7 +223,7 @@ def test_tx_leg_cpu_callable(mode, cfg):
         cur, peak = tracemalloc.get_traced_memory()
     finally:
         tracemalloc.stop()
-    assert peak - base < 4096 and abs(cur - base) < 4096, (peak - base, cur - base)
+    assert peak - base < 16384 and abs(cur - base) < 16384, (peak - base, cur - base)
     got = fn.arrays
     if mode == "build":                       # the closure's private copy, built in place
         out, _ = oracle.build_batch(hb.frames, hb.n, r, 3, **kw)

@@ -155,3 +155,29 @@ def test_icmp_gre_sums_in_plain_parse(torch, lead):
     db = engine.DeviceBatch.from_host(hb)
     c = engine.parse_batch_compact(db, 3).cpu().numpy().view(np.uint8).reshape(-1, 16)
     assert np.array_equal(c[:, 14:16].copy().view("<u2").reshape(-1), oracle_records(hb, 3)["l4_sum"])
+
+
+def test_tunnel_views_over_device_records(torch):
+    """rpkt_amd.tunviews over the GPU's records of the tunnel captures reads as the
+    reference's tests do (vlan_mpls_tests.rs:224-251, gtpv1_test.rs:199-231,
+    gre_test.rs:20-44)."""
+    from rpkt_amd.tunviews import Gre, Gtpv1, TunnelPacket, Vxlan
+    from rpkt_amd.views import EtherFrame, IpProtocol, Ipv4, Udp
+    names = ("Vxlan1.dat", "gtp-u-1ext.dat", "GREv0_1.dat")
+    frames = [oracle.load_dat(os.path.join(PKTS, n)) for n in names]
+    hb = host_batch(frames)
+    db = engine.DeviceBatch.from_host(hb)
+    go, gt, gi = (x.cpu().numpy() for x in engine.parse_tunnel_batch(db, F6))
+    go, gi, gt = as_records(go), as_records(gi), as_tunnels(gt)
+    pk = [TunnelPacket(go[k], gt[k], gi[k], frames[k]) for k in range(3)]
+    ip = [Ipv4.parse(EtherFrame.parse(p).unwrap().payload()).unwrap() for p in pk]
+    vx = Vxlan.parse(Udp.parse(ip[0].payload()).unwrap().payload()).unwrap()
+    assert vx.vni() == 3000001 and vx.group_id() == 100 and vx.reserved_4() == 0
+    assert Ipv4.parse(EtherFrame.parse(vx.payload()).unwrap().payload()).unwrap().verify_checksum()
+    gtp = Gtpv1.parse(Udp.parse(ip[1].payload()).unwrap().payload()).unwrap()
+    assert gtp.teid() == 1 and gtp.sequence() == 10461 and gtp.packet_len() == 100
+    assert Ipv4.parse(gtp.t_pdu()).unwrap().protocol() == IpProtocol.ICMP
+    gre = Gre.parse(ip[2].payload()).unwrap()
+    assert gre.checksum() == 30719 and gre.offset() == 0 and gre.verify_checksum()
+    inner = Ipv4.parse(gre.payload()).unwrap()
+    assert inner.ttl() == 64 and inner.ident() == 0x4c0f

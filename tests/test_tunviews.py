@@ -1,0 +1,102 @@
+"""The host tunnel views (rpkt_amd/tunviews.py) over the oracle's tunnel records, walked
+as the reference's tests walk their captures, with the same asserts
+(rpkt/tests/vlan_mpls_tests.rs:224-251, gtpv1_test.rs:199-231, 468-505,
+gre_test.rs:20-99)."""
+import os
+
+import pytest
+
+from oracle import oracle
+from rpkt_amd.records import F_IPV6
+from rpkt_amd.tunviews import Gre, Gtpv1, TunnelPacket, Vxlan
+from rpkt_amd.views import EtherFrame, EtherType, IpProtocol, Ipv4, Tcp, Udp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKTS = os.path.join(HERE, "golden", "packets")
+
+
+def packet(name, flags=3 | F_IPV6):
+    f = oracle.load_dat(os.path.join(PKTS, name))
+    o, t, i = oracle.tunnel_one(f, flags)
+    return TunnelPacket(o, t, i, f)
+
+
+def test_vxlan1_chain():
+    """vlan_mpls_tests.rs:224-251, assert for assert."""
+    eth_pkt = EtherFrame.parse(packet("Vxlan1.dat")).unwrap()
+    assert eth_pkt.ethertype() == EtherType.IPV4
+    ip_pkt = Ipv4.parse(eth_pkt.payload()).unwrap()
+    assert ip_pkt.protocol() == IpProtocol.UDP
+    udp_pkt = Udp.parse(ip_pkt.payload()).unwrap()
+    assert udp_pkt.dst_port() == 4789 and udp_pkt.src_port() == 45149
+    vxlan_pkt = Vxlan.parse(udp_pkt.payload()).unwrap()
+    assert vxlan_pkt.gbp_extention() and vxlan_pkt.vni_present()
+    assert vxlan_pkt.dont_learn() and vxlan_pkt.policy_applied()
+    assert (vxlan_pkt.reserved_0(), vxlan_pkt.reserved_1(), vxlan_pkt.reserved_2(),
+            vxlan_pkt.reserved_3(), vxlan_pkt.reserved_4()) == (0, 0, 0, 0, 0)
+    assert vxlan_pkt.group_id() == 100 and vxlan_pkt.vni() == 3000001
+    eth_pkt = EtherFrame.parse(vxlan_pkt.payload()).unwrap()
+    assert eth_pkt.ethertype() == EtherType.IPV4
+    # beyond the reference test: the inner IPv4 header and its sum, from the inner record
+    inner_ip = Ipv4.parse(eth_pkt.payload()).unwrap()
+    assert inner_ip.protocol() == IpProtocol.ICMP and inner_ip.verify_checksum()
+
+
+def test_gtp_u1_ext_chain():
+    """gtpv1_test.rs:199-231: the GTPv1 getters, then the T-PDU (the reference walks
+    ExtPduNumber::parse(gtp.payload()) -> Ipv4::parse(ext.payload()))."""
+    eth = EtherFrame.parse(packet("gtp-u-1ext.dat")).unwrap()
+    assert eth.ethertype() == EtherType.IPV4
+    ipv4 = Ipv4.parse(eth.payload()).unwrap()
+    assert ipv4.protocol() == IpProtocol.UDP
+    udp = Udp.parse(ipv4.payload()).unwrap()
+    assert udp.src_port() == 2152 and udp.dst_port() == 2152
+    gtp = Gtpv1.parse(udp.payload()).unwrap()
+    assert gtp.extention_header_present() and gtp.sequence_present() and not gtp.npdu_present()
+    assert gtp.message_type() == 255                                   # G_PDU
+    assert gtp.packet_len() == 92 + 8 and gtp.teid() == 1 and gtp.sequence() == 10461
+    assert gtp.next_extention_header() == 0xc0                         # PDU_NUMBER
+    assert gtp.payload().cursor() == gtp.buf.cursor() + 12             # the extension header
+    ipv4 = Ipv4.parse(gtp.t_pdu()).unwrap()
+    assert ipv4.protocol() == IpProtocol.ICMP and ipv4.verify_checksum()
+
+
+def test_gtp_pdu_session_container_chain():
+    """gtpv1_test.rs:468-505: no sequence, teid 14872, then IPv4 / TCP inside."""
+    eth = EtherFrame.parse(packet("gtp_pdu_session_container.dat")).unwrap()
+    udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
+    gtp = Gtpv1.parse(udp.payload()).unwrap()
+    assert gtp.teid() == 14872 and gtp.extention_header_present()
+    ipv4 = Ipv4.parse(gtp.t_pdu()).unwrap()
+    assert ipv4.protocol() == IpProtocol.TCP
+    tcp = Tcp.parse(ipv4.payload()).unwrap()
+    assert tcp.payload().cursor() > tcp.buf.cursor()
+
+
+def test_grev0_1_chain():
+    """gre_test.rs:20-44, assert for assert."""
+    eth = EtherFrame.parse(packet("GREv0_1.dat")).unwrap()
+    ipv4 = Ipv4.parse(eth.payload()).unwrap()
+    assert ipv4.protocol() == IpProtocol.GRE
+    gre = Gre.parse(ipv4.payload()).unwrap()
+    assert gre.header_len() == 8 and gre.checksum_present() and not gre.routing_present()
+    assert not gre.sequence_present() and gre.recursion_control() == 0 and gre.flags() == 0
+    assert gre.protocol_type() == EtherType.IPV4
+    assert gre.checksum() == 30719 and gre.offset() == 0
+    assert gre.verify_checksum()                                       # beyond the test
+    ipv4 = Ipv4.parse(gre.payload()).unwrap()
+    assert ipv4.ttl() == 64 and ipv4.ident() == 0x4c0f
+
+
+def test_views_refuse_what_the_engine_did_not_decode():
+    """Err where the reference parse fails or the dispatch does not reach the view: a
+    non-tunnel UDP payload, the wrong tunnel kind, a cursor elsewhere."""
+    eth = EtherFrame.parse(packet("Vxlan1.dat")).unwrap()
+    udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
+    assert Gtpv1.parse(udp.payload()).is_err() and Gre.parse(udp.payload()).is_err()
+    assert Vxlan.parse(eth.payload()).is_err()
+    eth = EtherFrame.parse(packet("gtp-c1.dat")).unwrap()
+    udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
+    assert Gtpv1.parse(udp.payload()).is_err()                         # GTP-C: no tunnel
+    with pytest.raises(ValueError):
+        Vxlan.parse(TunnelPacket(*oracle.tunnel_one(b"\0" * 20))).unwrap()
