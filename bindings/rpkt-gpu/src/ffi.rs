@@ -237,6 +237,18 @@ pub struct rpkt_tun_t {
 }
 const _: () = assert!(core::mem::size_of::<rpkt_tun_t>() == RPKT_TUN_BYTES);
 
+/// One slot of a ring of tunnelled bursts (rpkt_gpu_parse_tunnel_ring): a batch, its outer,
+/// tunnel and inner records and (with RPKT_F_FLOW_EV) its flow events.
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct rpkt_tun_ring_slot_t {
+    pub batch: rpkt_batch_t,
+    pub outer_dev: *mut rpkt_rec_t,
+    pub tun_dev: *mut rpkt_tun_t,
+    pub inner_dev: *mut rpkt_rec_t,
+    pub flow_ev_dev: *mut rpkt_flow_ev_t,
+}
+
 /// One frame's protocol stack from the pktfmt-derived walk, 64 bytes.
 #[repr(C)]
 #[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
@@ -347,6 +359,10 @@ extern "C" {
                                        inner_dev: *mut rpkt_rec_t,
                                        flow_ev_dev: *mut rpkt_flow_ev_t, n_buckets: u32,
                                        stream: *mut c_void) -> c_int;
+    /// Every slot parsed as by rpkt_gpu_parse_tunnel_batch, RPKT_RING_MAX_SLOTS slots per
+    /// launch.
+    pub fn rpkt_gpu_parse_tunnel_ring(slots: *const rpkt_tun_ring_slot_t, n_slots: u32,
+                                      flags: u32, n_buckets: u32, stream: *mut c_void) -> c_int;
     pub fn rpkt_gpu_build_tunnel_batch(batch: *const rpkt_batch_t, recs_dev: *const rpkt_rec_t,
                                        tun_dev: *const rpkt_tun_t, flags: u32, built_dev: *mut u8,
                                        stream: *mut c_void) -> c_int;

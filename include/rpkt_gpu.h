@@ -482,6 +482,23 @@ int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* batch, uint32_t flags, rpkt_
                                 rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev,
                                 rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream);
 
+/* A receive ring of tunnelled bursts (a VTEP's / UPF's rx queue: the loopback_rx.rs:96-121
+ * loop with the tunnel views of vlan_mpls_tests.rs:237-251 / gtpv1_test.rs:199-231 on
+ * each frame) in one launch per RPKT_RING_MAX_SLOTS slots: results equal one
+ * rpkt_gpu_parse_tunnel_batch call per slot, into that slot's outer_dev / tun_dev /
+ * inner_dev (and flow_ev_dev when RPKT_F_FLOW_EV is set).  Slots with n == 0 are skipped;
+ * every slot is checked before anything is launched; layouts may differ from slot to
+ * slot. */
+typedef struct rpkt_tun_ring_slot {
+    rpkt_batch_t    batch;
+    rpkt_rec_t*     outer_dev;
+    rpkt_tun_t*     tun_dev;
+    rpkt_rec_t*     inner_dev;
+    rpkt_flow_ev_t* flow_ev_dev;
+} rpkt_tun_ring_slot_t;
+int rpkt_gpu_parse_tunnel_ring(const rpkt_tun_ring_slot_t* slots, uint32_t n_slots,
+                               uint32_t flags, uint32_t n_buckets, void* stream);
+
 /* ---- TX side ---------------------------------------------------------------- */
 
 /* Build flags: fill a checksum the way the NIC TX offload requested by the

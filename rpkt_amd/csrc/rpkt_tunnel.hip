@@ -467,6 +467,59 @@ void tunnel_kernel(const uint8_t* __restrict__ frames, uint32_t fb,
                     inner, flow_ev, n_buckets, p0, lane);
 }
 
+// A ring of tunnelled bursts in one launch (rpkt_gpu_parse_tunnel_ring): wave t takes
+// tile t of the ring's tiles, numbered slot after slot (tile0[k] = the first tile of slot
+// k), and parses it exactly as tunnel_kernel parses that tile of the slot's own batch.  The
+// slot descriptors are kernel arguments (2.2 KB), read with scalar loads.
+constexpr uint32_t kTunRingMax = RPKT_RING_MAX_SLOTS;
+struct TunRingSlot {
+    const uint8_t* frames;
+    const uint32_t* offsets;
+    rpkt_rec_t* outer;
+    rpkt_tun_t* tun;
+    rpkt_rec_t* inner;
+    uint64_t* flow_ev;
+    uint32_t frames_bytes, stride, frame_len, n;
+};
+struct TunRingArgs {
+    uint32_t n_slots;
+    uint32_t tile0[kTunRingMax + 1];
+    TunRingSlot s[kTunRingMax];
+};
+
+template <bool L4>
+__global__ __launch_bounds__(kWave, 2)
+void tunnel_ring_kernel(const TunRingArgs A, uint32_t flags, uint32_t n_buckets) {
+    __shared__ __attribute__((aligned(16))) WaveScratch scratch;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t t = blockIdx.x;
+    if (t >= A.tile0[A.n_slots]) return;                         // wave-uniform exit
+    uint32_t k = 0;                                               // the slot holding tile t
+    for (uint32_t j = 1; j < A.n_slots; ++j) k = A.tile0[j] <= t ? j : k;
+    const TunRingSlot& S = A.s[k];
+    tunnel_tile<L4>(scratch, S.frames, S.frames_bytes, S.offsets, S.stride, S.frame_len, S.n,
+                    flags, S.outer, S.tun, S.inner, S.flow_ev, n_buckets,
+                    (t - A.tile0[k]) * kWave, lane);
+}
+
+constexpr uint32_t kTunFlags = RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_IPV6 | RPKT_F_FLOW_EV;
+
+// one batch's argument checks (rpkt_gpu_parse_tunnel_batch's, and each slot's of a ring):
+// 1 = launch it, else the status to return
+int tunnel_args_ok(const rpkt_batch_t& b, uint32_t flags, const void* outer, const void* tun,
+                   const void* inner, const void* flow_ev, uint32_t n_buckets) {
+    if (flags & RPKT_F_FLOW_EV) {
+        if (!flow_ev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS) return RPKT_E_INVAL;
+        if (((uintptr_t)flow_ev & 7u) != 0) return RPKT_E_ALIGN;
+    }
+    if (b.n == 0) return RPKT_OK;
+    if (!b.frames_dev || !outer || !tun || !inner) return RPKT_E_INVAL;
+    if (b.frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
+    if (!b.offsets_dev && b.stride == 0) return RPKT_E_INVAL;
+    if (((uintptr_t)outer | (uintptr_t)tun | (uintptr_t)inner) & 15u) return RPKT_E_ALIGN;
+    return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -475,23 +528,59 @@ int rpkt_gpu_parse_tunnel_batch(const rpkt_batch_t* b, uint32_t flags, rpkt_rec_
                                 rpkt_tun_t* tun_dev, rpkt_rec_t* inner_dev,
                                 rpkt_flow_ev_t* flow_ev_dev, uint32_t n_buckets, void* stream) {
     if (!b) return RPKT_E_INVAL;
-    if (flags & ~(uint32_t)(RPKT_F_IP_SUM | RPKT_F_L4_SUM | RPKT_F_IPV6 | RPKT_F_FLOW_EV))
-        return RPKT_E_INVAL;
-    if (flags & RPKT_F_FLOW_EV) {
-        if (!flow_ev_dev || n_buckets == 0 || n_buckets > RPKT_FLOW_MAX_BUCKETS) return RPKT_E_INVAL;
-        if (((uintptr_t)flow_ev_dev & 7u) != 0) return RPKT_E_ALIGN;
-    }
-    if (b->n == 0) return RPKT_OK;
-    if (!b->frames_dev || !outer_dev || !tun_dev || !inner_dev) return RPKT_E_INVAL;
-    if (b->frames_bytes > kMaxFrameBytes) return RPKT_E_TOO_LARGE;
-    if (!b->offsets_dev && b->stride == 0) return RPKT_E_INVAL;
-    if (((uintptr_t)outer_dev | (uintptr_t)tun_dev | (uintptr_t)inner_dev) & 15u) return RPKT_E_ALIGN;
+    if (flags & ~kTunFlags) return RPKT_E_INVAL;
+    const int ok = tunnel_args_ok(*b, flags, outer_dev, tun_dev, inner_dev, flow_ev_dev, n_buckets);
+    if (ok != 1) return ok;
     const uint32_t flen = b->offsets_dev ? 0 : (b->frame_len ? b->frame_len : b->stride);
     const uint32_t grid = (b->n + kWave - 1) / kWave;
     auto k = (flags & RPKT_F_L4_SUM) ? tunnel_kernel<true> : tunnel_kernel<false>;
     return launch(k, dim3(grid), dim3(kWave), 0, (hipStream_t)stream, b->frames_dev,
                   (uint32_t)b->frames_bytes, b->offsets_dev, b->stride, flen, b->n, flags, outer_dev,
                   tun_dev, inner_dev, (uint64_t*)flow_ev_dev, n_buckets);
+}
+
+int rpkt_gpu_parse_tunnel_ring(const rpkt_tun_ring_slot_t* slots, uint32_t n_slots,
+                               uint32_t flags, uint32_t n_buckets, void* stream) {
+    if (n_slots && !slots) return RPKT_E_INVAL;
+    if (flags & ~kTunFlags) return RPKT_E_INVAL;
+    for (uint32_t k = 0; k < n_slots; ++k) {                      // all checked, then launched
+        const rpkt_tun_ring_slot_t& q = slots[k];
+        if (q.batch.n == 0) continue;
+        const int ok = tunnel_args_ok(q.batch, flags, q.outer_dev, q.tun_dev, q.inner_dev,
+                                      q.flow_ev_dev, n_buckets);
+        if (ok != 1) return ok;
+    }
+    const bool fev = (flags & RPKT_F_FLOW_EV) != 0;
+    auto kern = (flags & RPKT_F_L4_SUM) ? tunnel_ring_kernel<true> : tunnel_ring_kernel<false>;
+    TunRingArgs A;
+    uint32_t k0 = 0;
+    while (k0 < n_slots) {
+        A.n_slots = 0;
+        A.tile0[0] = 0;
+        for (; k0 < n_slots && A.n_slots < kTunRingMax; ++k0) {
+            const rpkt_tun_ring_slot_t& q = slots[k0];
+            const rpkt_batch_t& b = q.batch;
+            if (b.n == 0) continue;
+            TunRingSlot& S = A.s[A.n_slots];
+            S.frames = b.frames_dev;
+            S.offsets = b.offsets_dev;
+            S.outer = q.outer_dev;
+            S.tun = q.tun_dev;
+            S.inner = q.inner_dev;
+            S.flow_ev = fev ? (uint64_t*)q.flow_ev_dev : nullptr;
+            S.frames_bytes = (uint32_t)b.frames_bytes;
+            S.stride = b.stride;
+            S.frame_len = b.offsets_dev ? 0u : (b.frame_len ? b.frame_len : b.stride);
+            S.n = b.n;
+            A.tile0[A.n_slots + 1] = A.tile0[A.n_slots] + (b.n + kWave - 1) / kWave;
+            ++A.n_slots;
+        }
+        if (A.n_slots == 0) break;
+        const int rc = launch(kern, dim3(A.tile0[A.n_slots]), dim3(kWave), 0, (hipStream_t)stream,
+                              A, flags, n_buckets);
+        if (rc) return rc;
+    }
+    return RPKT_OK;
 }
 
 }  // extern "C"

@@ -42,6 +42,12 @@ class RingSlot(ctypes.Structure):
     _fields_ = [("batch", Batch), ("recs_dev", ctypes.c_void_p), ("flow_ev_dev", ctypes.c_void_p)]
 
 
+class TunRingSlot(ctypes.Structure):
+    """rpkt_tun_ring_slot_t"""
+    _fields_ = [("batch", Batch), ("outer_dev", ctypes.c_void_p), ("tun_dev", ctypes.c_void_p),
+                ("inner_dev", ctypes.c_void_p), ("flow_ev_dev", ctypes.c_void_p)]
+
+
 class Fwd(ctypes.Structure):
     """rpkt_fwd_t"""
     _fields_ = [("dmac", ctypes.c_uint8 * 6), ("smac", ctypes.c_uint8 * 6),
@@ -60,7 +66,8 @@ EXPORTS = ["rpkt_gpu_abi_version", "rpkt_gpu_build_info", "rpkt_gpu_status_name"
            "rpkt_gpu_parse_options_batch", "rpkt_gpu_parse_options_batch_compact",
            "rpkt_gpu_parse_ring", "rpkt_gpu_parse_ring_compact", "rpkt_gpu_coll_unique_id",
            "rpkt_gpu_comm_init", "rpkt_gpu_comm_destroy", "rpkt_gpu_comm_init_timeout",
-           "rpkt_gpu_comm_abort", "rpkt_gpu_parse_tunnel_batch", "rpkt_gpu_build_tunnel_batch"]
+           "rpkt_gpu_comm_abort", "rpkt_gpu_parse_tunnel_batch", "rpkt_gpu_build_tunnel_batch",
+           "rpkt_gpu_parse_tunnel_ring"]
 COLL_ID_BYTES = 128
 
 _lib = None
@@ -138,6 +145,9 @@ def lib():
                                                   ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_uint32, ctypes.c_void_p]
         L.rpkt_gpu_parse_tunnel_batch.restype = ctypes.c_int
+        L.rpkt_gpu_parse_tunnel_ring.argtypes = [ctypes.POINTER(TunRingSlot), ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.rpkt_gpu_parse_tunnel_ring.restype = ctypes.c_int
         L.rpkt_gpu_build_tunnel_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_uint32,
                                                   ctypes.c_void_p, ctypes.c_void_p]
@@ -285,6 +295,40 @@ def parse_tunnel_batch(batch, flags=3, outer=None, tun=None, inner=None, stream=
                                            n_buckets, _stream_ptr(stream))
     _check(rc, "rpkt_gpu_parse_tunnel_batch")
     return (outer, tun, inner, flow_ev) if flags & F_FLOW_EV else (outer, tun, inner)
+
+
+def tunnel_ring_slots(batches, outers, tuns, inners, flow_evs=None):
+    """The rpkt_tun_ring_slot_t array of a ring of tunnelled bursts: batch k with its outer
+    record, tunnel record and inner record tensors (n * 80, n * 16, n * 80 bytes) and
+    (optional) its flow-event tensor.  As ring_slots: build it once, keep the tensors alive
+    and in place while it is used."""
+    k = len(batches)
+    if not (len(outers) == len(tuns) == len(inners) == k) or \
+            (flow_evs is not None and len(flow_evs) != k):
+        raise RpktError("tunnel_ring_slots: %d batches, %d/%d/%d record tensors"
+                        % (k, len(outers), len(tuns), len(inners)))
+    arr = (TunRingSlot * k)()
+    for j, db in enumerate(batches):
+        for t, per, what in ((outers[j], REC_BYTES, "outer"), (tuns[j], 16, "tunnel"),
+                             (inners[j], REC_BYTES, "inner")):
+            if t.numel() * t.element_size() < db.n * per:
+                raise RpktError("tunnel_ring_slots: slot %d %s records too small" % (j, what))
+        if flow_evs is not None and flow_evs[j].numel() * flow_evs[j].element_size() < 8 * db.n:
+            raise RpktError("tunnel_ring_slots: slot %d flow-event tensor too small" % j)
+        arr[j].batch = db.desc()
+        arr[j].outer_dev = outers[j].data_ptr()
+        arr[j].tun_dev = tuns[j].data_ptr()
+        arr[j].inner_dev = inners[j].data_ptr()
+        arr[j].flow_ev_dev = flow_evs[j].data_ptr() if flow_evs is not None else None
+    return arr
+
+
+def parse_tunnel_ring(slots, flags=3, n_buckets=0, stream=None):
+    """rpkt_gpu_parse_tunnel_ring: every slot of `slots` (tunnel_ring_slots()) parsed as by
+    parse_tunnel_batch, RPKT_RING_MAX_SLOTS slots per kernel launch."""
+    rc = lib().rpkt_gpu_parse_tunnel_ring(slots, len(slots), flags, n_buckets,
+                                          _stream_ptr(stream))
+    _check(rc, "rpkt_gpu_parse_tunnel_ring")
 
 
 def parse_batch_compact(batch, flags=3, recs=None, flow_ev=None, n_buckets=0, stream=None):
