@@ -10,7 +10,8 @@ Per seed: (a) a random packed or strided layout over the captures, configs 2/3/5
 the dual-stack fuzz (config 12) frames: the parse with a random flag set (with or without
 RPKT_F_IPV6) and flow events, compact records, a two-slot receive ring (80-B and compact),
 both option-walk entry points over full and compact records, the tunnel parse (the pool
-holds tunnel fuzz and tests/tunnel_frames.py frames), the layer walk; (b) a generator batch of a random config and size: the
+holds tunnel fuzz and tests/tunnel_frames.py frames) and a two-slot tunnel ring (this layout
+and a config 13 / 14 batch), the layer walk; (b) a generator batch of a random config and size: the
 build with random checksum flags over its (IPv4 and IPv6) records, the forward with and
 without RPKT_F_IPV6, and the encapsulation build over a tunnel batch (configs 13 / 14); (c)
 a fuzzed mbuf-chain batch (configs 8 / 12) through the chain
@@ -105,7 +106,23 @@ def check_layout(hb, rng):
     assert_same(as_records(gi.cpu().numpy()), oi)
     assert np.array_equal(gev.cpu().numpy().view(np.uint64),
                           oracle.tunnel_flow_events(oo, ot, oi, nb)), "tunnel flow events"
-    gl = engine.layers_batch(db).cpu().numpy().view(LAYERS_DTYPE)
+    # a ring of tunnelled bursts: this layout and a tunnel generator batch as two slots
+    hb3 = gen.make_batch(int(rng.choice([13, 14])), int(rng.integers(1, 3000)),
+                         seed=int(rng.integers(1, 1 << 30)))
+    dbs = [db, engine.DeviceBatch.from_host(hb3)]
+    outs = [[torch.empty(h.n * b, dtype=torch.uint8, device="cuda") for b in (80, 16, 80)] +
+            [torch.zeros(h.n, dtype=torch.int64, device="cuda")] for h in (hb, hb3)]
+    engine.parse_tunnel_ring(engine.tunnel_ring_slots(dbs, *[[x[j] for x in outs] for j in range(4)]),
+                             tf | F_FLOW_EV, nb)
+    for k, h in enumerate((hb, hb3)):
+        wo, wt, wi = (oo, ot, oi) if k == 0 else oracle.tunnel_batch(
+            h.frames, h.n, tf, offsets=h.offsets, stride=h.stride, frame_len=h.frame_len)
+        assert_same(as_records(outs[k][0].cpu().numpy()), wo)
+        assert as_tunnels(outs[k][1].cpu().numpy()).tobytes() == wt.tobytes(), "ring tunnel records"
+        assert_same(as_records(outs[k][2].cpu().numpy()), wi)
+        assert np.array_equal(outs[k][3].cpu().numpy().view(np.uint64),
+                              oracle.tunnel_flow_events(wo, wt, wi, nb)), "ring tunnel flow events"
+    gl =engine.layers_batch(db).cpu().numpy().view(LAYERS_DTYPE)
     ol = oracle.layers_batch(hb.frames, hb.n, offsets=hb.offsets, stride=hb.stride,
                              frame_len=hb.frame_len)
     assert gl.tobytes() == ol.tobytes(), "layer walk"
