@@ -12,8 +12,10 @@ tunnel API, so a receive loop written against rpkt's chain reads the same:
 The reference views and the chains its tests walk:
   Vxlan     rpkt/src/vxlan/generated.rs:17-103 (getters :45-84, payload :97-103)
   Gtpv1     rpkt/src/gtpv1/generated.rs:17-120, 233-290 (header_len, sequence, npdu,
-            next_extention_header); its extension headers' chain to the T-PDU
-            (gtpv1_test.rs:199-231) is `Gtpv1.t_pdu()` here
+            next_extention_header); its extension headers (ExtPduNumber, ExtUdpPort,
+            ExtLongPduNumber, ExtServiceClassIndicator, ExtContainer, PduSessionUp's
+            Dl/UlPduSessionInfo: :319-1517) walk to the T-PDU as gtpv1_test.rs:199-231,
+            284-320, 468-505 do; `Gtpv1.t_pdu()` jumps there directly
   Gre       rpkt/src/gre/generated.rs:17-110, 222-280 (checksum, offset, key, sequence)
 Ok / Err follow the engine's decode (rpkt_tun_t.kind / status): `parse` is Ok exactly
 where the reference parse returned Ok for this frame.  Getters come from the tunnel
@@ -215,6 +217,176 @@ class Gtpv1(_Tunnel):
         return Cursor(self.buf.rec, self.buf.frame, "raw", 0, at, max(0, end - at))
 
 
+class _GtpExt:
+    """A GTP-U extension header in the chain Gtpv1.payload() starts (gtpv1/generated.rs
+    :319-1300), read from the frame bytes as views.py reads IPv6 extension headers: the
+    engine walked the same chain to find the T-PDU (rpkt_tun_t.inner_off).  FIXED is the
+    view's fixed header length; variable-length headers are 4 * byte 0 long; the next
+    extension type is the header's last byte.  payload() advances header_len; the cursor it
+    returns is the T-PDU's (Ipv4 / Ipv6 parse from it) where the engine found the inner
+    packet, else a raw cursor the next extension header parses from."""
+    FIXED = 4
+    VARIABLE = False
+
+    def __init__(self, buf):
+        self.buf = buf
+        self.h = _frame_bytes(buf, buf.off, buf.length)
+
+    @classmethod
+    def parse(cls, buf):
+        """Err iff chunk_len < FIXED (and, variable-length, header_len < FIXED or
+        header_len > chunk_len), or the cursor is not one the chain reached."""
+        if buf.stage != "raw" or _tun(buf) is None or buf.frame is None or buf.length < cls.FIXED:
+            return Err(buf)
+        v = cls(buf)
+        if cls.VARIABLE and not (cls.FIXED <= v.header_len() <= buf.length):
+            return Err(buf)
+        return Ok(v)
+
+    def header_len(self):
+        return self.h[0] * 4 if self.VARIABLE else self.FIXED
+
+    def len(self):
+        return self.h[0]
+
+    def next_extention_header(self):
+        return self.h[self.header_len() - 1]
+
+    def payload(self):
+        b, t, hl = self.buf, _tun(self.buf), self.header_len()
+        if int(t["status"]) == TUN_STATUS["OK"] and b.off + hl == int(t["inner_off"]):
+            return _inner_cursor(b, t)
+        return Cursor(b.rec, b.frame, "raw", 0, b.off + hl, b.length - hl)
+
+
+class ExtUdpPort(_GtpExt):
+    """gtpv1/generated.rs:319-366 (type 0x40)."""
+
+    def udp_port(self):
+        return int.from_bytes(self.h[1:3], "big")
+
+
+class ExtPduNumber(_GtpExt):
+    """gtpv1/generated.rs:444-492 (type 0xc0)."""
+
+    def pdcp_number(self):
+        return int.from_bytes(self.h[1:3], "big")
+
+
+class ExtLongPduNumber(_GtpExt):
+    """gtpv1/generated.rs:570-634 (types 0x03 / 0x82)."""
+    FIXED = 8
+
+    def spare1(self):
+        return self.h[1] >> 2
+
+    def pdu_number(self):
+        return int.from_bytes(self.h[1:4], "big") & 0x3ffff
+
+    def spare2(self):
+        return self.h[4]
+
+    def spare3(self):
+        return self.h[5]
+
+    def spare4(self):
+        return self.h[6]
+
+
+class ExtServiceClassIndicator(_GtpExt):
+    """gtpv1/generated.rs:730-782 (type 0x20)."""
+
+    def service_class_indicator(self):
+        return self.h[1]
+
+    def spare(self):
+        return self.h[2]
+
+
+class ExtContainer(_GtpExt):
+    """gtpv1/generated.rs:863-935: any container (RAN / Xw RAN / NR RAN / PDU session,
+    types 0x81 / 0x83 / 0x84 / 0x85) as its length-prefixed bytes."""
+    FIXED = 1
+    VARIABLE = True
+
+    def var_header_slice(self):
+        return self.h[1:self.header_len()]
+
+
+class DlPduSessionInfo(_GtpExt):
+    """gtpv1/generated.rs:1029-1130: the PDU session container, PDU type 0."""
+    FIXED = 3
+    VARIABLE = True
+
+    def pdu_type(self):
+        return self.h[1] >> 4
+
+    def qmp(self):
+        return bool(self.h[1] & 0x8)
+
+    def snp(self):
+        return bool(self.h[1] & 0x4)
+
+    def msnp(self):
+        return bool(self.h[1] & 0x2)
+
+    def spare(self):
+        return self.h[1] & 0x1
+
+    def ppp(self):
+        return bool(self.h[2] & 0x80)
+
+    def rqi(self):
+        return bool(self.h[2] & 0x40)
+
+    def qos_flow_identifier(self):
+        return self.h[2] & 0x3f
+
+
+class UlPduSessionInfo(_GtpExt):
+    """gtpv1/generated.rs:1268-1330: the PDU session container, PDU type 1."""
+    FIXED = 3
+    VARIABLE = True
+
+    def pdu_type(self):
+        return self.h[1] >> 4
+
+    def qmp(self):
+        return (self.h[1] >> 3) & 1
+
+    def dl_delay_ind(self):
+        return (self.h[1] >> 2) & 1
+
+    def ul_delay_ind(self):
+        return (self.h[1] >> 1) & 1
+
+    def snp(self):
+        return self.h[1] & 1
+
+    def n3_n9_delay_ind(self):
+        return self.h[2] >> 7
+
+    def new_ie_flag(self):
+        return (self.h[2] >> 6) & 1
+
+    def qos_flow_identifier(self):
+        return self.h[2] & 0x3f
+
+
+class PduSessionUp:
+    """PduSessionUp::group_parse (gtpv1/generated.rs:1507-1517): dispatch on the PDU type
+    (byte 1 >> 4): 0 DlPduSessionInfo, 1 UlPduSessionInfo, else Err.  The Ok value is the
+    view itself (match on its class where rpkt matches the enum variant)."""
+
+    @staticmethod
+    def group_parse(buf):
+        if buf.stage != "raw" or buf.frame is None or buf.length < 2:
+            return Err(buf)
+        kind = _frame_bytes(buf, buf.off + 1, 1)[0] >> 4
+        cls = {0: DlPduSessionInfo, 1: UlPduSessionInfo}.get(kind)
+        return cls.parse(buf) if cls else Err(buf)
+
+
 class Gre(_Tunnel):
     """gre/generated.rs:17-110, 222-280 in an IPv4 / IPv6 payload (protocol 47)."""
     KIND = TUN_KIND["GRE"]
@@ -282,4 +454,6 @@ class Gre(_Tunnel):
         return int(self.buf.rec["l4_sum"]) == 0xffff
 
 
-__all__ = ["TunnelPacket", "Vxlan", "Gtpv1", "Gre"]
+__all__ = ["TunnelPacket", "Vxlan", "Gtpv1", "Gre", "ExtUdpPort", "ExtPduNumber",
+           "ExtLongPduNumber", "ExtServiceClassIndicator", "ExtContainer", "DlPduSessionInfo",
+           "UlPduSessionInfo", "PduSessionUp"]

@@ -161,7 +161,7 @@ def test_tunnel_views_over_device_records(torch):
     """rpkt_amd.tunviews over the GPU's records of the tunnel captures reads as the
     reference's tests do (vlan_mpls_tests.rs:224-251, gtpv1_test.rs:199-231,
     gre_test.rs:20-44)."""
-    from rpkt_amd.tunviews import Gre, Gtpv1, TunnelPacket, Vxlan
+    from rpkt_amd.tunviews import ExtPduNumber, Gre, Gtpv1, TunnelPacket, Vxlan
     from rpkt_amd.views import EtherFrame, IpProtocol, Ipv4, Udp
     names = ("Vxlan1.dat", "gtp-u-1ext.dat", "GREv0_1.dat")
     frames = [oracle.load_dat(os.path.join(PKTS, n)) for n in names]
@@ -177,6 +177,9 @@ def test_tunnel_views_over_device_records(torch):
     gtp = Gtpv1.parse(Udp.parse(ip[1].payload()).unwrap().payload()).unwrap()
     assert gtp.teid() == 1 and gtp.sequence() == 10461 and gtp.packet_len() == 100
     assert Ipv4.parse(gtp.t_pdu()).unwrap().protocol() == IpProtocol.ICMP
+    ext = ExtPduNumber.parse(gtp.payload()).unwrap()               # gtpv1_test.rs:224-231
+    assert ext.pdcp_number() == 2308 and ext.next_extention_header() == 0
+    assert Ipv4.parse(ext.payload()).unwrap().protocol() == IpProtocol.ICMP
     gre = Gre.parse(ip[2].payload()).unwrap()
     assert gre.checksum() == 30719 and gre.offset() == 0 and gre.verify_checksum()
     inner = Ipv4.parse(gre.payload()).unwrap()

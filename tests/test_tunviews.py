@@ -8,7 +8,8 @@ import pytest
 
 from oracle import oracle
 from rpkt_amd.records import F_IPV6
-from rpkt_amd.tunviews import Gre, Gtpv1, TunnelPacket, Vxlan
+from rpkt_amd.tunviews import (ExtContainer, ExtPduNumber, ExtUdpPort, Gre, Gtpv1, PduSessionUp,
+                               TunnelPacket, UlPduSessionInfo, Vxlan)
 from rpkt_amd.views import EtherFrame, EtherType, IpProtocol, Ipv4, Tcp, Udp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -57,8 +58,25 @@ def test_gtp_u1_ext_chain():
     assert gtp.packet_len() == 92 + 8 and gtp.teid() == 1 and gtp.sequence() == 10461
     assert gtp.next_extention_header() == 0xc0                         # PDU_NUMBER
     assert gtp.payload().cursor() == gtp.buf.cursor() + 12             # the extension header
-    ipv4 = Ipv4.parse(gtp.t_pdu()).unwrap()
+    ext = ExtPduNumber.parse(gtp.payload()).unwrap()
+    assert ext.pdcp_number() == 2308 and ext.next_extention_header() == 0   # NO_EXTENTION
+    ipv4 = Ipv4.parse(ext.payload()).unwrap()
     assert ipv4.protocol() == IpProtocol.ICMP and ipv4.verify_checksum()
+    assert Ipv4.parse(gtp.t_pdu()).unwrap().buf.cursor() == ipv4.buf.cursor()
+
+
+def test_gtp_u2_ext_chain():
+    """gtpv1_test.rs:284-320: ExtPduNumber -> ExtUdpPort -> the T-PDU."""
+    eth = EtherFrame.parse(packet("gtp-u-2ext.dat")).unwrap()
+    udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
+    gtp = Gtpv1.parse(udp.payload()).unwrap()
+    assert gtp.next_extention_header() == 0xc0                         # PDU_NUMBER
+    ext = ExtPduNumber.parse(gtp.payload()).unwrap()
+    assert ext.pdcp_number() == 2308 and ext.next_extention_header() == 0x40   # UDP_PORT
+    assert Ipv4.parse(ext.payload()).is_err()                          # not the T-PDU yet
+    ext = ExtUdpPort.parse(ext.payload()).unwrap()
+    assert ext.udp_port() == 1308 and ext.next_extention_header() == 0
+    assert Ipv4.parse(ext.payload()).unwrap().verify_checksum()
 
 
 def test_gtp_pdu_session_container_chain():
@@ -67,10 +85,32 @@ def test_gtp_pdu_session_container_chain():
     udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
     gtp = Gtpv1.parse(udp.payload()).unwrap()
     assert gtp.teid() == 14872 and gtp.extention_header_present()
-    ipv4 = Ipv4.parse(gtp.t_pdu()).unwrap()
+    assert gtp.packet_len() == 159 + 8 and gtp.next_extention_header() == 0x85
+    pkt = PduSessionUp.group_parse(gtp.payload()).unwrap()
+    assert isinstance(pkt, UlPduSessionInfo)
+    assert pkt.qos_flow_identifier() == 1 and pkt.next_extention_header() == 0
+    assert pkt.header_len() == 4
+    ipv4 = Ipv4.parse(pkt.payload()).unwrap()
     assert ipv4.protocol() == IpProtocol.TCP
     tcp = Tcp.parse(ipv4.payload()).unwrap()
     assert tcp.payload().cursor() > tcp.buf.cursor()
+
+
+def test_gtp_nr_container_chain():
+    """gtpv1_test.rs:377-416: a G-PDU carrying only an NR RAN container (no T-PDU: the
+    engine's tunnel status is not OK, the views still walk the header chain); the
+    container's payload is empty."""
+    eth = EtherFrame.parse(packet("gtp_nr_container.dat")).unwrap()
+    udp = Udp.parse(Ipv4.parse(eth.payload()).unwrap().payload()).unwrap()
+    gtp = Gtpv1.parse(udp.payload()).unwrap()
+    assert not gtp.sequence_present() and gtp.packet_len() == 16 + 8 and gtp.teid() == 1
+    assert gtp.next_extention_header() == 0x84                         # NR_RAN_CONTAINER
+    c = ExtContainer.parse(gtp.payload()).unwrap()
+    assert c.next_extention_header() == 0 and c.payload().remaining() == 0
+    v = c.var_header_slice()              # DlDataDeliveryStatus (generated.rs:1802-1890)
+    assert v[0] >> 4 == 1 and (v[0] >> 3) & 1 == 1                    # PDU type, highest_trans_nr_pdcp_sn_ind
+    assert int.from_bytes(v[2:6], "big") == 0                          # buf_size_for_data_radio_bearer
+    assert ExtPduNumber.parse(c.payload()).is_err()
 
 
 def test_grev0_1_chain():
