@@ -124,9 +124,10 @@ def build_gen(force=False):
     return GEN_LIB
 
 
-EXAMPLES = ("parse_batch", "flow_reduce", "rx_graph")
+EXAMPLES = ("parse_batch", "flow_reduce", "rx_graph", "vtep_rx")
 EXAMPLE_BIN = os.path.join(ROOT, "examples", "parse_batch")
 FLOW_REDUCE_BIN = os.path.join(ROOT, "examples", "flow_reduce")
+VTEP_RX_BIN = os.path.join(ROOT, "examples", "vtep_rx")
 
 
 def build_example(force=False):
