@@ -106,6 +106,46 @@ def test_captured_ring_call(torch):
         assert torch.equal(a, b)
 
 
+def test_captured_tunnel_ring(torch):
+    """A VTEP / UPF receive pass captured as one graph: a ring of tunnelled bursts
+    (configs 13 and 14) parsed by one rpkt_gpu_parse_tunnel_ring call with flow events,
+    then one flow count of the inner flows; replayed, it gives the oracle's records and
+    `passes` times the oracle's counters."""
+    nb, passes = 977, 3
+    hbs = [gen.make_batch(13 if k % 2 == 0 else 14, 700 + 433 * k, seed=1800 + k) for k in range(5)]
+    ring = [engine.DeviceBatch.from_host(h) for h in hbs]
+    n_ev = sum(h.n for h in hbs)
+    offs = np.cumsum([0] + [h.n for h in hbs])
+    outs = [[torch.empty(h.n * b, dtype=torch.uint8, device="cuda") for b in (80, 16, 80)]
+            for h in hbs]
+    ev_all = torch.empty(n_ev, dtype=torch.int64, device="cuda")
+    slots = engine.tunnel_ring_slots(ring, *[[x[j] for x in outs] for j in range(3)],
+                                     [ev_all[offs[k]:offs[k + 1]] for k in range(len(hbs))])
+    cnt = torch.zeros((nb + 1) * 4, dtype=torch.int64, device="cuda")
+    ws = engine.flow_workspace(n_ev, nb)
+    flags = 3 | engine.F_FLOW_EV
+
+    def rx_pass():
+        engine.parse_tunnel_ring(slots, flags, nb)
+        engine.flow_count(ev_all, n_ev, nb, counters=cnt, workspace=ws)
+
+    loop = graphs.CapturedLoop(rx_pass)
+    for _ in range(passes - 1):
+        loop.replay()
+    torch.cuda.synchronize()
+    want_ev = []
+    for k, hb in enumerate(hbs):
+        oo, ot, oi = oracle.tunnel_batch(hb.frames, hb.n, 3, offsets=hb.offsets, stride=hb.stride,
+                                         frame_len=hb.frame_len)
+        for got, w in zip(outs[k], (oo, ot, oi)):
+            assert got.cpu().numpy().tobytes() == w.tobytes(), "slot %d" % k
+        want_ev.append(oracle.tunnel_flow_events(oo, ot, oi, nb))
+    want_ev = np.concatenate(want_ev)
+    assert np.array_equal(ev_all.cpu().numpy().view(np.uint64), want_ev)
+    want = oracle.flow_count(want_ev, nb) * np.uint64(passes)
+    assert np.array_equal(cnt.cpu().numpy().view(np.uint64), want)
+
+
 def test_replay_reads_refilled_slots(torch):
     """The graph bakes in buffer addresses, not contents: a slot refilled between replays
     (as a NIC refills its ring) is parsed from its new frames."""
