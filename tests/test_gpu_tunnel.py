@@ -99,6 +99,16 @@ def test_tunnel_odd_frames(torch, lead):
         check_tunnel(hb, flags)
 
 
+@pytest.mark.parametrize("lead", [0, 3, 9])
+def test_tunnel_jumbo_frames(torch, lead):
+    """Tunnelled jumbo frames to 60 KB of inner payload (VXLAN over IPv4 / IPv6, GRE with
+    its checksum, GTP-U with extension headers) and cuts of them: the long streams, the
+    tail lines of joint tiles and the outer sums that reuse the inner stream."""
+    hb = host_batch(tf.jumbo_frames(seed=lead, n=48 + lead), lead)
+    for flags in (3, F6, 1):
+        check_tunnel(hb, flags)
+
+
 def test_tunnel_empty_batch_and_validation(torch):
     hb = host_batch([b""])
     db = engine.DeviceBatch.from_host(hb)

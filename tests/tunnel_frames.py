@@ -118,3 +118,27 @@ def odd_frames(seed=0, n=64):
                 f[int(rng.integers(34, len(f)))] = int(rng.integers(0, 256))
         out.append(bytes(f))
     return out
+
+
+def jumbo_frames(seed=0, n=48):
+    """Tunnelled jumbo frames (inner payloads of 1.4 KB to 60 KB: the long-stream and
+    tail-line paths of the tunnel parse), mixed with short tunnel frames, and cuts of them."""
+    rng = np.random.default_rng(seed)
+    base = []
+    for p in (1400, 8950, 16000, 60000):
+        inner = inner_udp4(p)
+        base.append(ether(0x0800, ipv4_packet(17, udp(40000, 4789, vxlan(ether(0x0800, inner))))))
+        base.append(ether(0x0800, ipv4_packet(47, gre(inner, checksum=True, key=9))))
+        if p <= 30000:
+            base.append(ether(0x0800, ipv4_packet(17, udp(2152, 2152, gtpu(
+                inner, [(0xc0, b"\x09\x04"), (0x85, bytes([0x10, 1]))], seq=5)))))
+            base.append(ether(0x86dd, ipv6_packet(17, udp(40000, 4789, vxlan(ether(0x0800, inner))))))
+    base.append(ether(0x0800, ipv4_packet(17, udp(40000, 4789, vxlan(ether(0x0800, inner_udp4(40)))))))
+    out = list(base)
+    while len(out) < n:
+        f = bytes(base[int(rng.integers(len(base)))])
+        if rng.integers(2):
+            f = f[:int(rng.integers(0, len(f) + 1))]
+        out.append(f)
+    order = rng.permutation(len(out))
+    return [out[k] for k in order]
