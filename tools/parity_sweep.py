@@ -51,6 +51,7 @@ def extend_pool():
         p += fuzz_layouts.frames_of(gen.make_batch(11, 40, seed=111))
         p += fuzz_layouts.frames_of(gen.make_batch(14, 600, seed=141))     # tunnel fuzz
         p += tunnel_frames.odd_frames(seed=7, n=200)
+        p += tunnel_frames.jumbo_frames(seed=5, n=24)                       # to 60 KB inner
         extend_pool.done = True
 
 
