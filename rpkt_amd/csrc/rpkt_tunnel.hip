@@ -317,10 +317,11 @@ __device__ __forceinline__ uint64_t record_event(const WordsT& w, uint32_t n_buc
     return flow_event(R, x, n_buckets);
 }
 
-// chunk loads in flight per lane in the main stream (6 and 8 measured: no gain, and 8 costs
-// occupancy)
+// chunk loads in flight per lane in the main stream (2: 1-2 % faster than 3 and 4, the
+// fewer lines in flight the fewer window lines evicted before their reuse; 6 and 8: no gain,
+// and 8 costs occupancy)
 #ifndef RPKT_TUN_UNROLL
-#define RPKT_TUN_UNROLL 4
+#define RPKT_TUN_UNROLL 2
 #endif
 constexpr int kTunUnroll = RPKT_TUN_UNROLL;
 
